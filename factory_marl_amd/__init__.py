@@ -1,0 +1,11 @@
+"""factory_marl_amd -- MI355X-native batched env-step path of nkirschi/Factory-MARL.
+
+The reference steps one MuJoCo arena per Python process (challenge_env BaseEnv.step_sim +
+src/environments.py wrappers, driven by SB3 SubprocVecEnv).  Here every arena lives in HBM and one
+hand-written HIP kernel (csrc/fm_kernel.hip) advances all of them per env-step; FactoryVecEnv exposes
+the SB3 VecEnv surface over it.  See DESIGN.md.
+"""
+from ._lib import FactorySimError, load  # noqa: F401
+from .vec_env import FactoryVecEnv  # noqa: F401
+
+__all__ = ["FactoryVecEnv", "FactorySimError", "load"]

@@ -1,0 +1,112 @@
+"""ctypes binding of libfactorysim.so (the C ABI in include/factorysim.h).
+
+The product path is the HIP library only: if ``libfactorysim.so`` is missing or cannot be loaded this
+module raises -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfactorysim.so")
+
+FM_ENV_FACTORY_SCORE = 0
+FM_ENV_ALLFULLRL_PROGRESS = 1
+FM_FP32 = 0
+FM_FP64 = 1
+
+
+class FmConfig(C.Structure):
+    _fields_ = [
+        ("num_arenas", C.c_int32),
+        ("num_arms", C.c_int32),
+        ("max_num_objects", C.c_int32),
+        ("env_class", C.c_int32),
+        ("precision", C.c_int32),
+        ("max_contacts", C.c_int32),
+        ("initial_conveyor_speed", C.c_double),
+        ("conveyor_acceleration", C.c_double),
+        ("pt_time", C.c_double),
+        ("force_contact_threshold", C.c_double),
+        ("control_frequency", C.c_double),
+        ("spawn_freq", C.c_double),
+        ("spawn_freq_increase", C.c_double),
+        ("gripper_to_closest_cube_reward_factor", C.c_double),
+        ("closest_cube_to_bucket_reward_factor", C.c_double),
+        ("small_action_norm_reward_factor", C.c_double),
+        ("base_reward", C.c_double),
+        ("solver_iterations", C.c_int32),
+        ("solver_tolerance", C.c_double),
+    ]
+
+
+class FmInfo(C.Structure):
+    _fields_ = [
+        ("scores", C.c_void_p),
+        ("num_obj", C.c_void_p),
+        ("play_time", C.c_void_p),
+        ("conveyor_speed", C.c_void_p),
+        ("out_of_reach", C.c_void_p),
+        ("force_terminate", C.c_void_p),
+        ("terminal_obs", C.c_void_p),
+        ("episode_return", C.c_void_p),
+        ("episode_length", C.c_void_p),
+        ("terminal_scores", C.c_void_p),
+    ]
+
+
+EXPORTED = [
+    "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
+    "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_reset", "fm_step", "fm_state_size",
+    "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump",
+]
+
+_LIB = None
+
+
+class FactorySimError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (raises if it is missing: the product has no fallback path)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise FactorySimError(f"{LIB_PATH} not built: run `python __graft_entry__.py build` (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    P, I = C.c_void_p, C.c_int
+    L.fm_config_default.argtypes = [C.POINTER(FmConfig)]
+    L.fm_config_default.restype = None
+    L.fm_create.argtypes = [C.POINTER(FmConfig), I, C.POINTER(C.c_uint64), C.POINTER(P)]
+    L.fm_create.restype = I
+    L.fm_destroy.argtypes = [P]
+    L.fm_destroy.restype = None
+    L.fm_last_error.argtypes = []
+    L.fm_last_error.restype = C.c_char_p
+    L.fm_set_stream.argtypes = [P, P]
+    L.fm_set_stream.restype = I
+    L.fm_sync.argtypes = [P]
+    L.fm_sync.restype = I
+    for n in ["fm_obs_dim", "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_state_size"]:
+        getattr(L, n).argtypes = [P]
+        getattr(L, n).restype = I
+    L.fm_reset.argtypes = [P, P, P]
+    L.fm_reset.restype = I
+    L.fm_step.argtypes = [P, P, P, P, P, P, C.POINTER(FmInfo)]
+    L.fm_step.restype = I
+    L.fm_get_state.argtypes = [P, P]
+    L.fm_get_state.restype = I
+    L.fm_set_state.argtypes = [P, P]
+    L.fm_set_state.restype = I
+    L.fm_get_counters.argtypes = [P, P]
+    L.fm_get_counters.restype = I
+    L.fm_debug_dump.argtypes = [P, I, I, P, I]
+    L.fm_debug_dump.restype = I
+    _LIB = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise FactorySimError(f"factorysim error {rc}: {load().fm_last_error().decode()}")

@@ -1,0 +1,2735 @@
+// fm_kernel.hip -- the MI355X env-step pipeline: one workgroup (= one 64-lane wavefront) per arena.
+//
+// One launch advances every arena by one env-step of the reference
+// (FactoryManipulationEnv.step -> BaseEnv.step_sim, environments.py:151-202, base_env.py:240-282):
+//   AllFullRL action transform (environments.py:84-102, 481-495) and ctrl clipping (base_env.py:255-262)
+//   frame_skip (=100) x [ low-pass ctrl target (base_env.py:209-215) ; dm_control legacy physics.step()
+//                         = mj_step2 (actuation, smooth acceleration, Newton constraint solve, implicitfast
+//                           integration) ; mj_step1 (FK, inertia, collision, constraints, bias forces) ]
+//   contact-force termination (base_env.py:225-236), TaskManager.step (task_utils.py:131-144),
+//   speed / spawn-rate updates (base_env.py:266-270), progress or score reward (environments.py:129-149,
+//   342-383), observation (environments.py:55-82), SB3-style auto-reset (reset_sim, base_env.py:177-198).
+// The arena's whole working set (state, body poses, contacts, Jacobian blocks, Newton Hessian) lives in
+// LDS for the duration of the env-step; HBM is touched only for the per-arena state record, the
+// action / observation rows and the (L2-resident) scene tables.
+//
+// Lane mapping: sequential chains run on few lanes (one lane per arm for FK + RNE, lane 0 for the task
+// layer); everything with natural width runs across the wave (geoms, broadphase pairs, narrowphase,
+// contact rows, Hessian entries, Cholesky trailing updates, line-search reductions).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/factorysim.h"
+#include "fm_dev.hpp"
+#include "fm_scene.hpp"
+
+namespace fm {
+
+#define LANE ((int)threadIdx.x)
+#define SYNC() __syncthreads()
+
+template <typename T>
+struct Ws {
+  char* base;
+  const Lay* L;
+  __device__ T* q() const { return (T*)(base + L->q); }
+  __device__ T* v() const { return (T*)(base + L->v); }
+  __device__ T* a() const { return (T*)(base + L->a); }
+  __device__ T* as() const { return (T*)(base + L->as); }
+  __device__ T* fs() const { return (T*)(base + L->fs); }
+  __device__ T* fc() const { return (T*)(base + L->fc); }
+  __device__ T* pb() const { return (T*)(base + L->pb); }
+  __device__ T* g() const { return (T*)(base + L->g); }
+  __device__ T* dir() const { return (T*)(base + L->dir); }
+  __device__ T* Ma() const { return (T*)(base + L->Ma); }
+  __device__ T* tmp() const { return (T*)(base + L->tmp); }
+  __device__ T* fa() const { return (T*)(base + L->fa); }
+  __device__ double* ctrl() const { return (double*)(base + L->ctrl); }
+  __device__ T* alen() const { return (T*)(base + L->alen); }
+  __device__ T* avel() const { return (T*)(base + L->avel); }
+  __device__ T* aforce() const { return (T*)(base + L->aforce); }
+  __device__ T* bpos() const { return (T*)(base + L->bpos); }
+  __device__ T* bR() const { return (T*)(base + L->bR); }
+  __device__ T* bcom() const { return (T*)(base + L->bcom); }
+  __device__ T* bIw() const { return (T*)(base + L->bIw); }
+  __device__ T* bF() const { return (T*)(base + L->bF); }
+  __device__ T* bN() const { return (T*)(base + L->bN); }
+  __device__ T* dax() const { return (T*)(base + L->dax); }
+  __device__ T* danc() const { return (T*)(base + L->danc); }
+  __device__ T* site() const { return (T*)(base + L->site); }
+  __device__ T* cR() const { return (T*)(base + L->cR); }
+  __device__ T* Marm() const { return (T*)(base + L->Marm); }
+  __device__ T* Larm() const { return (T*)(base + L->Larm); }
+  __device__ T* LBarm() const { return (T*)(base + L->LBarm); }
+  __device__ T* gx() const { return (T*)(base + L->gx); }
+  __device__ T* gR() const { return (T*)(base + L->gR); }
+  __device__ T* H() const { return (T*)(base + L->H); }
+  __device__ int* ci() const { return (int*)(base + L->c_i); }
+  __device__ T* cr() const { return (T*)(base + L->c_r); }
+  __device__ int* ri() const { return (int*)(base + L->r_i); }
+  __device__ T* rr() const { return (T*)(base + L->r_r); }
+  __device__ uint16_t* surv() const { return (uint16_t*)(base + L->surv); }
+  __device__ uint64_t* tmask() const { return (uint64_t*)(base + L->tmask); }
+  __device__ int* misc() const { return (int*)(base + L->misc); }
+  __device__ int* sortidx() const { return (int*)(base + L->sort); }
+  __device__ double* uctl() const { return (double*)(base + L->uctl); }
+  __device__ double* scal() const { return (double*)(base + L->scal); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// tree / dof helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int tree_dof(const Dims& d, int t) {
+  return t == 0 ? 0 : (t <= d.K ? 1 + 6 * (t - 1) : 1 + 6 * d.K + 9 * (t - 1 - d.K));
+}
+__device__ __forceinline__ int tree_nd(const Dims& d, int t) { return t == 0 ? 1 : (t <= d.K ? 6 : 9); }
+__device__ __forceinline__ int kbody_tree(const Dims& d, int kb) {
+  if (kb == 0) return -1;
+  if (kb == 1) return 0;
+  if (kb < 2 + d.K) return kb - 1;
+  return 1 + d.K + (kb - 2 - d.K) / 10;
+}
+__device__ __forceinline__ int dof_tree(const Dims& d, int i) {
+  if (i == 0) return 0;
+  if (i < 1 + 6 * d.K) return 1 + (i - 1) / 6;
+  return 1 + d.K + (i - 1 - 6 * d.K) / 9;
+}
+
+// ------------------------------------------------------------------------------------------------
+// impedance / reference acceleration parameters (MuJoCo getimpedance, getKBIP with refsafe)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ T impedance(const T* si, T x) {
+  T dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
+  const T lo = T(0.0001), hi = T(0.9999);
+  dmin = dmin < lo ? lo : (dmin > hi ? hi : dmin);
+  dmax = dmax < lo ? lo : (dmax > hi ? hi : dmax);
+  if (dmin == dmax || width <= T(1e-15)) return T(0.5) * (dmin + dmax);
+  x = fabs(x) / width;
+  if (x >= T(1)) return dmax;
+  if (x <= T(0)) return dmin;
+  T y;
+  if (power == T(1))
+    y = x;
+  else if (x <= mid)
+    y = pow(x, power) / pow(mid, power - T(1));
+  else
+    y = T(1) - pow(T(1) - x, power) / pow(T(1) - mid, power - T(1));
+  return dmin + y * (dmax - dmin);
+}
+
+template <typename T>
+__device__ void kb_params(T dt, const T* solref, const T* solimp, T& K, T& B) {
+  T tc = solref[0], dr = solref[1];
+  T dmax = solimp[1];
+  dmax = dmax < T(0.0001) ? T(0.0001) : (dmax > T(0.9999) ? T(0.9999) : dmax);
+  if (tc > T(0)) {
+    if (tc < T(2) * dt) tc = T(2) * dt;
+    T k = dmax * dmax * tc * tc * dr * dr;
+    T b = dmax * tc;
+    K = T(1) / (k > T(1e-15) ? k : T(1e-15));
+    B = T(2) / (b > T(1e-15) ? b : T(1e-15));
+  } else {
+    K = -tc / (dmax * dmax);
+    B = -dr / dmax;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// narrowphase (definitions identical to oracle/collide.c; normal from geom1 to geom2)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+struct Con {
+  T dist, pos[3], n[3];
+};
+
+template <typename T>
+__device__ int np_plane_sphere(const T* c, T r, Con<T>* out) {
+  // floor plane: origin, normal +z (scene.xml:21)
+  T dist = c[2] - r;
+  if (dist > T(0)) return 0;
+  out[0].dist = dist;
+  out[0].n[0] = 0;
+  out[0].n[1] = 0;
+  out[0].n[2] = 1;
+  out[0].pos[0] = c[0];
+  out[0].pos[1] = c[1];
+  out[0].pos[2] = c[2] - (r + dist / T(2));
+  return 1;
+}
+
+template <typename T>
+__device__ int np_plane_box(const T* p, const T* R, const T* h, Con<T>* out) {
+  T dist = p[2];
+  int cnt = 0;
+  for (int i = 0; i < 8; i++) {
+    T cl[3] = {(i & 1) ? h[0] : -h[0], (i & 2) ? h[1] : -h[1], (i & 4) ? h[2] : -h[2]};
+    T cw[3];
+    matvec3(R, cl, cw);
+    T ld = cw[2];
+    if (dist + ld > T(0) || ld > T(0)) continue;
+    T cd = dist + ld;
+    out[cnt].dist = cd;
+    out[cnt].n[0] = 0;
+    out[cnt].n[1] = 0;
+    out[cnt].n[2] = 1;
+    out[cnt].pos[0] = cw[0] + p[0];
+    out[cnt].pos[1] = cw[1] + p[1];
+    out[cnt].pos[2] = cw[2] + p[2] - cd / T(2);
+    if (++cnt >= 4) return 4;
+  }
+  return cnt;
+}
+
+template <typename T>
+__device__ int np_sphere_sphere(const T* c1, T r1, const T* c2, T r2, Con<T>* out) {
+  T n[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  T len = sqrt(dot3(n, n));
+  T dist = len - r1 - r2;
+  if (dist > T(0)) return 0;
+  if (len < T(1e-15)) {
+    n[0] = 1;
+    n[1] = n[2] = 0;
+  } else {
+    for (int k = 0; k < 3; k++) n[k] /= len;
+  }
+  out[0].dist = dist;
+  for (int k = 0; k < 3; k++) {
+    out[0].n[k] = n[k];
+    out[0].pos[k] = c1[k] + n[k] * (r1 + dist / T(2));
+  }
+  return 1;
+}
+
+template <typename T>
+__device__ int np_sphere_box(const T* c, T r, const T* p, const T* R, const T* h, Con<T>* out) {
+  T d[3] = {c[0] - p[0], c[1] - p[1], c[2] - p[2]};
+  T pl[3];
+  mattvec3(R, d, pl);
+  T q[3];
+  bool inside = true;
+  for (int k = 0; k < 3; k++) {
+    q[k] = pl[k] < -h[k] ? -h[k] : (pl[k] > h[k] ? h[k] : pl[k]);
+    if (q[k] != pl[k]) inside = false;
+  }
+  T nl[3], dist;
+  if (!inside) {
+    T dl[3] = {q[0] - pl[0], q[1] - pl[1], q[2] - pl[2]};
+    T len = sqrt(dot3(dl, dl));
+    dist = len - r;
+    if (dist > T(0)) return 0;
+    for (int k = 0; k < 3; k++) nl[k] = dl[k] / len;
+  } else {
+    int best = 0;
+    T bd = h[0] - fabs(pl[0]);
+    for (int k = 1; k < 3; k++) {
+      T dk = h[k] - fabs(pl[k]);
+      if (dk < bd) {
+        bd = dk;
+        best = k;
+      }
+    }
+    nl[0] = nl[1] = nl[2] = 0;
+    nl[best] = pl[best] >= T(0) ? T(-1) : T(1);
+    dist = -bd - r;
+  }
+  T n[3];
+  matvec3(R, nl, n);
+  out[0].dist = dist;
+  for (int k = 0; k < 3; k++) {
+    out[0].n[k] = n[k];
+    out[0].pos[k] = c[k] + n[k] * (r + dist / T(2));
+  }
+  return 1;
+}
+
+template <typename T>
+__device__ int np_box_box(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2, const T* h2,
+                          Con<T>* out) {
+  T a[3][3], b[3][3];
+  for (int k = 0; k < 3; k++)
+    for (int r = 0; r < 3; r++) {
+      a[k][r] = R1[3 * r + k];
+      b[k][r] = R2[3 * r + k];
+    }
+  T d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  T best_face = T(1e30), best_edge = T(1e30);
+  int face_id = -1, edge_id = -1;
+  T face_u[3] = {0, 0, 0}, edge_u[3] = {0, 0, 0};
+  T face_s = 0, edge_s = 0;
+  for (int ax = 0; ax < 15; ax++) {
+    T u[3];
+    if (ax < 3) {
+      u[0] = a[ax][0];
+      u[1] = a[ax][1];
+      u[2] = a[ax][2];
+    } else if (ax < 6) {
+      u[0] = b[ax - 3][0];
+      u[1] = b[ax - 3][1];
+      u[2] = b[ax - 3][2];
+    } else {
+      int i = (ax - 6) / 3, j = (ax - 6) % 3;
+      cross3(a[i], b[j], u);
+      T n = sqrt(dot3(u, u));
+      if (n < T(1e-6)) continue;
+      for (int k = 0; k < 3; k++) u[k] /= n;
+    }
+    T ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) {
+      ra += h1[k] * fabs(dot3(u, a[k]));
+      rb += h2[k] * fabs(dot3(u, b[k]));
+    }
+    T s = dot3(u, d);
+    T ov = ra + rb - fabs(s);
+    if (ov < T(0)) return 0;
+    if (ax < 6) {
+      if (ov < best_face) {
+        best_face = ov;
+        face_id = ax;
+        face_u[0] = u[0];
+        face_u[1] = u[1];
+        face_u[2] = u[2];
+        face_s = s;
+      }
+    } else if (ov < best_edge) {
+      best_edge = ov;
+      edge_id = ax;
+      edge_u[0] = u[0];
+      edge_u[1] = u[1];
+      edge_u[2] = u[2];
+      edge_s = s;
+    }
+  }
+  if (edge_id >= 0 && best_edge < T(0.95) * best_face) {
+    T sg = edge_s >= T(0) ? T(1) : T(-1);
+    T n[3] = {edge_u[0] * sg, edge_u[1] * sg, edge_u[2] * sg};
+    int i = (edge_id - 6) / 3, j = (edge_id - 6) % 3;
+    T e1[3] = {p1[0], p1[1], p1[2]}, e2[3] = {p2[0], p2[1], p2[2]};
+    for (int k = 0; k < 3; k++) {
+      if (k != i) {
+        T sgn = dot3(n, a[k]) >= T(0) ? T(1) : T(-1);
+        for (int r = 0; r < 3; r++) e1[r] += h1[k] * sgn * a[k][r];
+      }
+      if (k != j) {
+        T sgn = dot3(n, b[k]) >= T(0) ? T(-1) : T(1);
+        for (int r = 0; r < 3; r++) e2[r] += h2[k] * sgn * b[k][r];
+      }
+    }
+    T w[3] = {e1[0] - e2[0], e1[1] - e2[1], e1[2] - e2[2]};
+    T bb = dot3(a[i], b[j]), dd = dot3(a[i], w), ee = dot3(b[j], w);
+    T den = T(1) - bb * bb;
+    T s = 0, t = 0;
+    if (den > T(1e-12)) {
+      s = (bb * ee - dd) / den;
+      t = (ee - bb * dd) / den;
+    }
+    s = s < -h1[i] ? -h1[i] : (s > h1[i] ? h1[i] : s);
+    t = t < -h2[j] ? -h2[j] : (t > h2[j] ? h2[j] : t);
+    out[0].dist = -best_edge;
+    for (int r = 0; r < 3; r++) {
+      out[0].n[r] = n[r];
+      out[0].pos[r] = T(0.5) * (e1[r] + s * a[i][r] + e2[r] + t * b[j][r]);
+    }
+    return 1;
+  }
+  T sg = face_s >= T(0) ? T(1) : T(-1);
+  T n[3] = {face_u[0] * sg, face_u[1] * sg, face_u[2] * sg};
+  const T *pr, *hr, *pi, *hi;
+  T nref[3];
+  int kr;
+  bool ref1 = face_id < 3;
+  if (ref1) {
+    pr = p1;
+    hr = h1;
+    pi = p2;
+    hi = h2;
+    kr = face_id;
+    nref[0] = n[0];
+    nref[1] = n[1];
+    nref[2] = n[2];
+  } else {
+    pr = p2;
+    hr = h2;
+    pi = p1;
+    hi = h1;
+    kr = face_id - 3;
+    nref[0] = -n[0];
+    nref[1] = -n[1];
+    nref[2] = -n[2];
+  }
+  T(*ar)[3] = ref1 ? a : b;
+  T(*ai)[3] = ref1 ? b : a;
+  T fc[3];
+  for (int k = 0; k < 3; k++) fc[k] = pr[k] + nref[k] * hr[kr];
+  int t1 = (kr + 1) % 3, t2 = (kr + 2) % 3;
+  int mi = 0;
+  T bestdot = T(-1);
+  for (int k = 0; k < 3; k++) {
+    T dk = fabs(dot3(nref, ai[k]));
+    if (dk > bestdot) {
+      bestdot = dk;
+      mi = k;
+    }
+  }
+  T sgn = dot3(nref, ai[mi]) > T(0) ? T(-1) : T(1);
+  T ic[3];
+  for (int k = 0; k < 3; k++) ic[k] = pi[k] + sgn * hi[mi] * ai[mi][k];
+  int u1 = (mi + 1) % 3, u2 = (mi + 2) % 3;
+  T poly[8][3], tmp[8][3];
+  const T sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
+  for (int vtx = 0; vtx < 4; vtx++)
+    for (int k = 0; k < 3; k++)
+      poly[vtx][k] = ic[k] + sx[vtx] * hi[u1] * ai[u1][k] + sy[vtx] * hi[u2] * ai[u2][k];
+  int np = 4;
+  for (int pl = 0; pl < 4 && np > 0; pl++) {
+    const T* t = ar[pl < 2 ? t1 : t2];
+    T e = hr[pl < 2 ? t1 : t2];
+    T sside = (pl & 1) ? T(-1) : T(1);
+    int nn = 0;
+    for (int vtx = 0; vtx < np; vtx++) {
+      const T* P = poly[vtx];
+      const T* Q = poly[(vtx + 1) % np];
+      T rp[3] = {P[0] - fc[0], P[1] - fc[1], P[2] - fc[2]};
+      T rq[3] = {Q[0] - fc[0], Q[1] - fc[1], Q[2] - fc[2]};
+      T dp = e - sside * dot3(rp, t);
+      T dq = e - sside * dot3(rq, t);
+      if (dp >= T(0) && nn < 8) {
+        tmp[nn][0] = P[0];
+        tmp[nn][1] = P[1];
+        tmp[nn][2] = P[2];
+        nn++;
+      }
+      if ((dp >= T(0)) != (dq >= T(0)) && nn < 8) {
+        T f = dp / (dp - dq);
+        for (int k = 0; k < 3; k++) tmp[nn][k] = P[k] + (Q[k] - P[k]) * f;
+        nn++;
+      }
+    }
+    np = nn;
+    for (int vtx = 0; vtx < nn; vtx++)
+      for (int k = 0; k < 3; k++) poly[vtx][k] = tmp[vtx][k];
+  }
+  int cnt = 0;
+  for (int vtx = 0; vtx < np && cnt < 8; vtx++) {
+    T rv[3] = {fc[0] - poly[vtx][0], fc[1] - poly[vtx][1], fc[2] - poly[vtx][2]};
+    T depth = dot3(rv, nref);
+    if (depth < T(0)) continue;
+    out[cnt].dist = -depth;
+    for (int k = 0; k < 3; k++) {
+      out[cnt].n[k] = n[k];
+      out[cnt].pos[k] = poly[vtx][k] + nref[k] * depth / T(2);
+    }
+    cnt++;
+  }
+  return cnt;
+}
+
+// ------------------------------------------------------------------------------------------------
+// stage (mj_step1): kinematics, inertia, bias forces, collision, constraint rows, efc velocities
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ void arm_chain(const Model<T>& M, const Ws<T>& w, int arm, bool with_dyn) {
+  const Dims& dm = M.dm;
+  const T* q = w.q() + 1 + 7 * dm.K + 9 * arm;
+  const T* qd = w.v() + 1 + 6 * dm.K + 9 * arm;
+  const T* base = M.arm_base + 12 * arm;
+  T* bpos = w.bpos() + 30 * arm;
+  T* bR = w.bR() + 90 * arm;
+  T* bcom = w.bcom() + 30 * arm;
+  T* bIw = w.bIw() + 60 * arm;
+  T* bF = w.bF() + 30 * arm;
+  T* bN = w.bN() + 30 * arm;
+  T* dax = w.dax() + 27 * arm;
+  T* danc = w.danc() + 27 * arm;
+  const T p0[3] = {base[0], base[1], base[2]};
+  // chain state of the current parent (link chain), saved state of the gripper base for the plates
+  T Pp[3] = {base[0], base[1], base[2]}, PR[9];
+  for (int k = 0; k < 9; k++) PR[k] = base[3 + k];
+  T Pw[3] = {0, 0, 0}, Pal[3] = {0, 0, 0}, Pvo[3] = {0, 0, 0}, Pao[3] = {0, 0, 0};
+  T Gp[3], GR[9], Gw[3], Gal[3], Gvo[3], Gao[3];
+  for (int b = 0; b < 10; b++) {
+    if (b >= 8) {  // both plates hang off the gripper base
+      for (int k = 0; k < 3; k++) {
+        Pp[k] = Gp[k];
+        Pw[k] = Gw[k];
+        Pal[k] = Gal[k];
+        Pvo[k] = Gvo[k];
+        Pao[k] = Gao[k];
+      }
+      for (int k = 0; k < 9; k++) PR[k] = GR[k];
+    }
+    const T* bl = M.body + 32 * b;
+    T off[3], Rpre[9];
+    matvec3(PR, bl, off);
+    matmul3(PR, bl + 3, Rpre);
+    T o[3] = {Pp[0] + off[0], Pp[1] + off[1], Pp[2] + off[2]};
+    T R[9];
+    T wv[3] = {Pw[0], Pw[1], Pw[2]}, al[3] = {Pal[0], Pal[1], Pal[2]};
+    T vo[3], ao[3];
+    if (b < 7) {
+      T ax[3] = {Rpre[2], Rpre[5], Rpre[8]};
+      for (int k = 0; k < 3; k++) {
+        dax[3 * b + k] = ax[k];
+        danc[3 * b + k] = o[k];
+      }
+      T c = cos(q[b]), s = sin(q[b]);
+      // R = Rpre * Rz(q)
+      for (int r = 0; r < 3; r++) {
+        R[3 * r + 0] = Rpre[3 * r + 0] * c + Rpre[3 * r + 1] * s;
+        R[3 * r + 1] = -Rpre[3 * r + 0] * s + Rpre[3 * r + 1] * c;
+        R[3 * r + 2] = Rpre[3 * r + 2];
+      }
+      if (with_dyn) {
+        T r[3] = {o[0] - Pp[0], o[1] - Pp[1], o[2] - Pp[2]};
+        T t1[3], t2[3], t3[3], wa[3];
+        cross3(Pw, r, t1);
+        cross3(Pal, r, t2);
+        cross3(Pw, t1, t3);
+        cross3(Pw, ax, wa);
+        for (int k = 0; k < 3; k++) {
+          vo[k] = Pvo[k] + t1[k];
+          ao[k] = Pao[k] + t2[k] + t3[k];
+          al[k] += wa[k] * qd[b];
+          wv[k] += ax[k] * qd[b];
+        }
+      }
+    } else if (b == 7) {
+      for (int k = 0; k < 9; k++) R[k] = Rpre[k];
+      if (with_dyn) {
+        T r[3] = {o[0] - Pp[0], o[1] - Pp[1], o[2] - Pp[2]};
+        T t1[3], t2[3], t3[3];
+        cross3(Pw, r, t1);
+        cross3(Pal, r, t2);
+        cross3(Pw, t1, t3);
+        for (int k = 0; k < 3; k++) {
+          vo[k] = Pvo[k] + t1[k];
+          ao[k] = Pao[k] + t2[k] + t3[k];
+        }
+      }
+    } else {
+      int d = b - 1;  // dof 7 (left plate, body 8) / 8 (right plate, body 9)
+      T ax[3] = {Rpre[0], Rpre[3], Rpre[6]};
+      for (int k = 0; k < 3; k++) o[k] += ax[k] * q[d];
+      for (int k = 0; k < 3; k++) {
+        dax[3 * d + k] = ax[k];
+        danc[3 * d + k] = o[k];
+      }
+      for (int k = 0; k < 9; k++) R[k] = Rpre[k];
+      if (with_dyn) {
+        T r[3] = {o[0] - Pp[0], o[1] - Pp[1], o[2] - Pp[2]};
+        T t1[3], t2[3], t3[3], wa[3];
+        cross3(Pw, r, t1);
+        cross3(Pal, r, t2);
+        cross3(Pw, t1, t3);
+        cross3(Pw, ax, wa);
+        for (int k = 0; k < 3; k++) {
+          vo[k] = Pvo[k] + t1[k] + ax[k] * qd[d];
+          ao[k] = Pao[k] + t2[k] + t3[k] + T(2) * wa[k] * qd[d];
+        }
+      }
+    }
+    for (int k = 0; k < 3; k++) bpos[3 * b + k] = o[k];
+    for (int k = 0; k < 9; k++) bR[9 * b + k] = R[k];
+    // com and world inertia
+    T ci[3];
+    matvec3(R, bl + 13, ci);
+    T com[3] = {o[0] + ci[0], o[1] + ci[1], o[2] + ci[2]};
+    for (int k = 0; k < 3; k++) bcom[3 * b + k] = com[k];
+    T Ri[9];
+    matmul3(R, bl + 16, Ri);
+    const T* I = bl + 25;
+    T Iw[6];
+    Iw[0] = Ri[0] * I[0] * Ri[0] + Ri[1] * I[1] * Ri[1] + Ri[2] * I[2] * Ri[2];
+    Iw[1] = Ri[3] * I[0] * Ri[3] + Ri[4] * I[1] * Ri[4] + Ri[5] * I[2] * Ri[5];
+    Iw[2] = Ri[6] * I[0] * Ri[6] + Ri[7] * I[1] * Ri[7] + Ri[8] * I[2] * Ri[8];
+    Iw[3] = Ri[0] * I[0] * Ri[3] + Ri[1] * I[1] * Ri[4] + Ri[2] * I[2] * Ri[5];
+    Iw[4] = Ri[0] * I[0] * Ri[6] + Ri[1] * I[1] * Ri[7] + Ri[2] * I[2] * Ri[8];
+    Iw[5] = Ri[3] * I[0] * Ri[6] + Ri[4] * I[1] * Ri[7] + Ri[5] * I[2] * Ri[8];
+    for (int k = 0; k < 6; k++) bIw[6 * b + k] = Iw[k];
+    if (with_dyn) {
+      T mass = bl[12];
+      T rc[3] = {com[0] - o[0], com[1] - o[1], com[2] - o[2]};
+      T u1[3], u2[3], u3[3];
+      cross3(al, rc, u1);
+      cross3(wv, rc, u2);
+      cross3(wv, u2, u3);
+      T F[3];
+      for (int k = 0; k < 3; k++) F[k] = mass * (ao[k] + u1[k] + u3[k]);
+      F[2] += mass * M.grav;
+      T Iwv[3] = {Iw[0] * wv[0] + Iw[3] * wv[1] + Iw[4] * wv[2], Iw[3] * wv[0] + Iw[1] * wv[1] + Iw[5] * wv[2],
+                  Iw[4] * wv[0] + Iw[5] * wv[1] + Iw[2] * wv[2]};
+      T Ial[3] = {Iw[0] * al[0] + Iw[3] * al[1] + Iw[4] * al[2], Iw[3] * al[0] + Iw[1] * al[1] + Iw[5] * al[2],
+                  Iw[4] * al[0] + Iw[5] * al[1] + Iw[2] * al[2]};
+      T gy[3];
+      cross3(wv, Iwv, gy);
+      T cr[3] = {com[0] - p0[0], com[1] - p0[1], com[2] - p0[2]}, mo[3];
+      cross3(cr, F, mo);
+      for (int k = 0; k < 3; k++) {
+        bF[3 * b + k] = F[k];
+        bN[3 * b + k] = mo[k] + Ial[k] + gy[k];
+      }
+    }
+    // advance the chain
+    for (int k = 0; k < 3; k++) Pp[k] = o[k];
+    for (int k = 0; k < 9; k++) PR[k] = R[k];
+    if (with_dyn) {
+      for (int k = 0; k < 3; k++) {
+        Pw[k] = wv[k];
+        Pal[k] = al[k];
+        Pvo[k] = vo[k];
+        Pao[k] = ao[k];
+      }
+    }
+    if (b == 7) {
+      for (int k = 0; k < 3; k++) {
+        Gp[k] = o[k];
+        Gw[k] = Pw[k];
+        Gal[k] = Pal[k];
+        Gvo[k] = Pvo[k];
+        Gao[k] = Pao[k];
+      }
+      for (int k = 0; k < 9; k++) GR[k] = R[k];
+      // between_gripper_plates site (gripper.xml:43)
+      T so[3] = {0, 0, T(0.05)}, sp[3];
+      matvec3(R, so, sp);
+      for (int k = 0; k < 3; k++) w.site()[3 * arm + k] = o[k] + sp[k];
+    }
+  }
+  if (with_dyn) {
+    // backward pass: generalized bias forces of the arm's 9 dofs (RNE, qacc = 0)
+    T* pb = w.pb() + 1 + 6 * dm.K + 9 * arm;
+    pb[7] = -(dax[21] * bF[24] + dax[22] * bF[25] + dax[23] * bF[26]);
+    pb[8] = -(dax[24] * bF[27] + dax[25] * bF[28] + dax[26] * bF[29]);
+    T ft[3] = {0, 0, 0}, nt[3] = {0, 0, 0};
+    for (int b = 9; b >= 0; b--) {
+      for (int k = 0; k < 3; k++) {
+        ft[k] += bF[3 * b + k];
+        nt[k] += bN[3 * b + k];
+      }
+      if (b <= 6) {
+        T ar[3] = {danc[3 * b] - p0[0], danc[3 * b + 1] - p0[1], danc[3 * b + 2] - p0[2]}, af[3];
+        cross3(ar, ft, af);
+        T tn[3] = {nt[0] - af[0], nt[1] - af[1], nt[2] - af[2]};
+        pb[b] = -dot3(dax + 3 * b, tn);
+      }
+    }
+  }
+}
+
+// column of the translational Jacobian of point p on arm body b for arm dof d (0 if not in chain)
+template <typename T>
+__device__ __forceinline__ void arm_jac_col(const Ws<T>& w, int arm, int b, int d, const T* p, T* col) {
+  const T* ax = w.dax() + 27 * arm + 3 * d;
+  bool in = d < 7 ? (b >= 7 || d <= b) : ((d == 7 && b == 8) || (d == 8 && b == 9));
+  if (!in) {
+    col[0] = col[1] = col[2] = 0;
+    return;
+  }
+  if (d < 7) {
+    const T* an = w.danc() + 27 * arm + 3 * d;
+    T rel[3] = {p[0] - an[0], p[1] - an[1], p[2] - an[2]};
+    cross3(ax, rel, col);
+  } else {
+    col[0] = ax[0];
+    col[1] = ax[1];
+    col[2] = ax[2];
+  }
+}
+
+// translational Jacobian column j (tree-local) of point p on kernel body kb in its tree
+template <typename T>
+__device__ void body_jac_col(const Model<T>& M, const Ws<T>& w, int kb, int j, const T* p, T* col) {
+  const Dims& dm = M.dm;
+  if (kb == 1) {
+    col[0] = 0;
+    col[1] = 1;
+    col[2] = 0;
+  } else if (kb < 2 + dm.K) {
+    int k = kb - 2;
+    if (j < 3) {
+      col[0] = col[1] = col[2] = 0;
+      col[j] = 1;
+    } else {
+      const T* R = w.cR() + 9 * k;
+      const T* c = w.q() + 1 + 7 * k;
+      T ax[3] = {R[j - 3], R[3 + j - 3], R[6 + j - 3]};
+      T rel[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+      cross3(ax, rel, col);
+    }
+  } else {
+    int arm = (kb - 2 - dm.K) / 10, b = (kb - 2 - dm.K) % 10;
+    arm_jac_col(w, arm, b, j, p, col);
+  }
+}
+
+template <typename T>
+__device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
+  const Dims& dm = M.dm;
+  const int A = dm.A, K = dm.K, nv = dm.nv;
+  T* q = w.q();
+  T* v = w.v();
+  // ---- kinematics + RNE (one lane per arm), cubes (one lane per cube)
+  if (LANE < A) arm_chain(M, w, LANE, true);
+  for (int k = LANE; k < K; k += WAVE) {
+    T* qq = q + 1 + 7 * k;
+    T qu[4] = {qq[3], qq[4], qq[5], qq[6]};
+    T n = sqrt(qu[0] * qu[0] + qu[1] * qu[1] + qu[2] * qu[2] + qu[3] * qu[3]);
+    if (n < T(1e-15)) {
+      qu[0] = 1;
+      qu[1] = qu[2] = qu[3] = 0;
+    } else if (fabs(n - T(1)) > T(1e-15)) {
+      for (int c = 0; c < 4; c++) qu[c] /= n;
+    }
+    T* R = w.cR() + 9 * k;
+    T ww = qu[0], x = qu[1], y = qu[2], z = qu[3];
+    R[0] = ww * ww + x * x - y * y - z * z;
+    R[1] = T(2) * (x * y - ww * z);
+    R[2] = T(2) * (x * z + ww * y);
+    R[3] = T(2) * (x * y + ww * z);
+    R[4] = ww * ww - x * x + y * y - z * z;
+    R[5] = T(2) * (y * z - ww * x);
+    R[6] = T(2) * (x * z - ww * y);
+    R[7] = T(2) * (y * z + ww * x);
+    R[8] = ww * ww - x * x - y * y + z * z;
+    // passive - bias of the free joint: gravity only (com at the body origin, isotropic inertia)
+    T* pb = w.pb() + 1 + 6 * k;
+    T m = M.cube[((size_t)arena * K + k) * 4 + 1];
+    pb[0] = 0;
+    pb[1] = 0;
+    pb[2] = -m * M.grav;
+    pb[3] = pb[4] = pb[5] = 0;
+  }
+  if (LANE == 0) w.pb()[0] = -M.belt_damp * v[0];  // belt: damping, no gravity along y
+  SYNC();
+  // ---- actuator length / velocity (transmission at the stage state)
+  for (int u = LANE; u < dm.nu; u += WAVE) {
+    T L, V;
+    if (u == 0) {
+      L = q[0];
+      V = v[0];
+    } else {
+      int arm = (u - 1) / 8, j = (u - 1) % 8;
+      int qa = 1 + 7 * K + 9 * arm, va = 1 + 6 * K + 9 * arm;
+      if (j < 7) {
+        L = q[qa + j];
+        V = v[va + j];
+      } else {
+        L = T(0.5) * q[qa + 7] + T(0.5) * q[qa + 8];
+        V = T(0.5) * v[va + 7] + T(0.5) * v[va + 8];
+      }
+    }
+    w.alen()[u] = L;
+    w.avel()[u] = V;
+  }
+  // ---- geom world poses of moving geoms
+  for (int g = LANE; g < dm.ngc; g += WAVE) {
+    const int* gi = M.geom_i + 4 * g;
+    int kb = gi[2], slot = gi[3];
+    if (kb == 0) continue;
+    const T* gg = M.geom + 16 * g;
+    T* gx = w.gx() + 3 * g;
+    if (kb == 1) {
+      gx[0] = 0;
+      gx[1] = q[0];
+      gx[2] = T(1.05);
+      T* R = w.gR() + 9 * slot;
+      for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? T(1) : T(0);
+    } else if (kb < 2 + K) {
+      int k = kb - 2;
+      for (int c = 0; c < 3; c++) gx[c] = q[1 + 7 * k + c];
+      T* R = w.gR() + 9 * slot;
+      for (int c = 0; c < 9; c++) R[c] = w.cR()[9 * k + c];
+    } else {
+      int arm = (kb - 2 - K) / 10, b = (kb - 2 - K) % 10;
+      const T* bp = w.bpos() + 30 * arm + 3 * b;
+      const T* bR = w.bR() + 90 * arm + 9 * b;
+      T off[3];
+      matvec3(bR, gg, off);
+      for (int c = 0; c < 3; c++) gx[c] = bp[c] + off[c];
+      if (slot >= 0) matmul3(bR, gg + 3, w.gR() + 9 * slot);
+    }
+  }
+  // ---- arm mass-matrix blocks: M_ij = sum_{b in desc} m Jc_i.Jc_j + Jr_i' Iw Jr_j
+  for (int e = LANE; e < 45 * A; e += WAVE) {
+    int arm = e / 45, t = e % 45;
+    int i = 0;
+    while (t > i) {
+      t -= i + 1;
+      i++;
+    }
+    int j = t;  // i >= j
+    int b0, b1;
+    if (i <= 6) {
+      b0 = i;
+      b1 = 9;
+    } else {
+      b0 = b1 = i + 1;
+    }
+    T s = 0;
+    const T* dax = w.dax() + 27 * arm;
+    for (int b = b0; b <= b1; b++) {
+      const T* com = w.bcom() + 30 * arm + 3 * b;
+      T ci[3], cj[3];
+      arm_jac_col(w, arm, b, i, com, ci);
+      arm_jac_col(w, arm, b, j, com, cj);
+      T mass = M.body[32 * b + 12];
+      s += mass * dot3(ci, cj);
+      if (i <= 6 && j <= 6) {
+        const T* Iw = w.bIw() + 60 * arm + 6 * b;
+        const T* ri = dax + 3 * i;
+        const T* rj = dax + 3 * j;
+        T Ir[3] = {Iw[0] * rj[0] + Iw[3] * rj[1] + Iw[4] * rj[2], Iw[3] * rj[0] + Iw[1] * rj[1] + Iw[5] * rj[2],
+                   Iw[4] * rj[0] + Iw[5] * rj[1] + Iw[2] * rj[2]};
+        s += dot3(ri, Ir);
+      }
+    }
+    T* Ma = w.Marm() + 81 * arm;
+    Ma[9 * i + j] = s;
+    Ma[9 * j + i] = s;
+  }
+  // ---- broadphase (bounding spheres) + narrowphase, in chunks of MAXSURV survivors
+  int* misc = w.misc();
+  if (LANE == 0) {
+    misc[MISC_NCON] = 0;
+    misc[MISC_NROW] = 0;
+  }
+  SYNC();
+  int start = 0;
+  while (start < dm.npair) {
+    int nsurv = 0;
+    int p = start;
+    for (; p < dm.npair && nsurv + WAVE <= MAXSURV; p += WAVE) {
+      int idx = p + LANE;
+      bool hit = false;
+      if (idx < dm.npair) {
+        uint32_t pw = M.pair[idx];
+        int c1 = pw & 4095, c2 = (pw >> 12) & 4095;
+        T r1 = M.geom[16 * c1 + 15], r2 = M.geom[16 * c2 + 15];
+        if (r1 > T(0) && r2 > T(0)) {
+          const T* x1 = w.gx() + 3 * c1;
+          const T* x2 = w.gx() + 3 * c2;
+          T d0 = x1[0] - x2[0], d1 = x1[1] - x2[1], d2 = x1[2] - x2[2];
+          T rs = r1 + r2;
+          hit = sqrt(d0 * d0 + d1 * d1 + d2 * d2) <= rs;
+        } else {
+          hit = true;  // planes: no bounding test (MuJoCo)
+        }
+      }
+      uint64_t bal = __ballot(hit);
+      int before = __popcll(bal & ((1ull << LANE) - 1ull));
+      if (hit) w.surv()[nsurv + before] = (uint16_t)idx;
+      nsurv += __popcll(bal);
+    }
+    start = p;
+    SYNC();
+    // narrowphase: one survivor pair per lane, contacts appended in pair order (wave prefix sum)
+    for (int s0 = 0; s0 < nsurv; s0 += WAVE) {
+      int sidx = s0 + LANE;
+      Con<T> cs[MAXPC];
+      int nc = 0;
+      int c1 = 0, c2 = 0;
+      if (sidx < nsurv) {
+        uint32_t pw = M.pair[w.surv()[sidx]];
+        c1 = pw & 4095;
+        c2 = (pw >> 12) & 4095;
+        int t1 = M.geom_i[4 * c1 + 1], t2 = M.geom_i[4 * c2 + 1];
+        const T* x1 = w.gx() + 3 * c1;
+        const T* x2 = w.gx() + 3 * c2;
+        if (t1 == GT_PLANE && t2 == GT_SPHERE) {
+          nc = np_plane_sphere(x2, M.geom[16 * c2 + 12], cs);
+        } else if (t1 == GT_PLANE && t2 == GT_BOX) {
+          T h[3];
+          if (M.geom_i[4 * c2 + 2] >= 2 && M.geom_i[4 * c2 + 2] < 2 + K) {
+            T hh = M.cube[((size_t)arena * K + (M.geom_i[4 * c2 + 2] - 2)) * 4];
+            h[0] = h[1] = h[2] = hh;
+          } else {
+            for (int k = 0; k < 3; k++) h[k] = M.geom[16 * c2 + 12 + k];
+          }
+          nc = np_plane_box(x2, w.gR() + 9 * M.geom_i[4 * c2 + 3], h, cs);
+        } else if (t1 == GT_SPHERE && t2 == GT_SPHERE) {
+          nc = np_sphere_sphere(x1, M.geom[16 * c1 + 12], x2, M.geom[16 * c2 + 12], cs);
+        } else if (t1 == GT_SPHERE && t2 == GT_BOX) {
+          T h[3];
+          if (M.geom_i[4 * c2 + 2] >= 2 && M.geom_i[4 * c2 + 2] < 2 + K) {
+            T hh = M.cube[((size_t)arena * K + (M.geom_i[4 * c2 + 2] - 2)) * 4];
+            h[0] = h[1] = h[2] = hh;
+          } else {
+            for (int k = 0; k < 3; k++) h[k] = M.geom[16 * c2 + 12 + k];
+          }
+          nc = np_sphere_box(x1, M.geom[16 * c1 + 12], x2, w.gR() + 9 * M.geom_i[4 * c2 + 3], h, cs);
+        } else if (t1 == GT_BOX && t2 == GT_BOX) {
+          T h1[3], h2[3];
+          int kb1 = M.geom_i[4 * c1 + 2], kb2 = M.geom_i[4 * c2 + 2];
+          for (int k = 0; k < 3; k++) {
+            h1[k] = M.geom[16 * c1 + 12 + k];
+            h2[k] = M.geom[16 * c2 + 12 + k];
+          }
+          if (kb1 >= 2 && kb1 < 2 + K) h1[0] = h1[1] = h1[2] = M.cube[((size_t)arena * K + kb1 - 2) * 4];
+          if (kb2 >= 2 && kb2 < 2 + K) h2[0] = h2[1] = h2[2] = M.cube[((size_t)arena * K + kb2 - 2) * 4];
+          nc = np_box_box(x1, w.gR() + 9 * M.geom_i[4 * c1 + 3], h1, x2, w.gR() + 9 * M.geom_i[4 * c2 + 3], h2,
+                          cs);
+        }
+      }
+      // exclusive prefix sum of nc over the wave
+      int incl = nc;
+#pragma unroll
+      for (int o = 1; o < WAVE; o <<= 1) {
+        int y = __shfl_up(incl, o);
+        if (LANE >= o) incl += y;
+      }
+      int total = __shfl(incl, WAVE - 1);
+      int base = misc[MISC_NCON];
+      int off = base + incl - nc;
+      for (int c = 0; c < nc; c++) {
+        int slot = off + c;
+        if (slot >= dm.maxcon) break;
+        int* ci = w.ci() + 4 * slot;
+        T* cr = w.cr() + CR_N * slot;
+        uint32_t pw = M.pair[w.surv()[sidx]];
+        ci[0] = (int)(pw & 0xFFFFFF);
+        ci[3] = (int)(pw >> 24);
+        cr[CR_DIST] = cs[c].dist;
+        for (int k = 0; k < 3; k++) {
+          cr[CR_POS + k] = cs[c].pos[k];
+          cr[CR_FR + k] = cs[c].n[k];
+        }
+      }
+      SYNC();
+      if (LANE == 0) {
+        int nt = base + total;
+        if (nt > dm.maxcon) {
+          ctr[0] += nt - dm.maxcon;
+          nt = dm.maxcon;
+        }
+        misc[MISC_NCON] = nt;
+      }
+      SYNC();
+    }
+  }
+  SYNC();
+  const int ncon = misc[MISC_NCON];
+  // ---- contact rows: frame, Jacobian blocks, impedance, D, reference-acceleration terms
+  for (int c = LANE; c < ncon; c += WAVE) {
+    int* ci = w.ci() + 4 * c;
+    T* cr = w.cr() + CR_N * c;
+    int c1 = ci[0] & 4095, c2 = (ci[0] >> 12) & 4095;
+    int pidx = ci[3];
+    int kb1 = M.geom_i[4 * c1 + 2], kb2 = M.geom_i[4 * c2 + 2];
+    int tr1 = kbody_tree(dm, kb1), tr2 = kbody_tree(dm, kb2);
+    int mj1 = M.geom_i[4 * c1], mj2 = M.geom_i[4 * c2];
+    int armflag = (mj1 >= 13 + K || mj2 >= 13 + K) ? 1 : 0;
+    // frame (mju_makeFrame)
+    T* f = cr + CR_FR;
+    T nn = sqrt(dot3(f, f));
+    if (nn < T(1e-15)) {
+      f[0] = 1;
+      f[1] = f[2] = 0;
+    } else {
+      f[0] /= nn;
+      f[1] /= nn;
+      f[2] /= nn;
+    }
+    f[3] = f[4] = f[5] = 0;
+    if (f[1] < T(0.5) && f[1] > T(-0.5))
+      f[4] = 1;
+    else
+      f[5] = 1;
+    T tt = dot3(f, f + 3);
+    for (int k = 0; k < 3; k++) f[3 + k] -= tt * f[k];
+    T n2 = sqrt(dot3(f + 3, f + 3));
+    if (n2 < T(1e-15)) {
+      f[3] = 1;
+      f[4] = f[5] = 0;
+    } else {
+      for (int k = 0; k < 3; k++) f[3 + k] /= n2;
+    }
+    cross3(f, f + 3, f + 6);
+    // Jacobian blocks B = frame * (J(body2) - J(body1)) on the contact point
+    int ta = -1, tb = -1;
+    if (tr1 >= 0) ta = tr1;
+    if (tr2 >= 0) {
+      if (ta < 0)
+        ta = tr2;
+      else if (tr2 != ta)
+        tb = tr2;
+    }
+    int nda = ta >= 0 ? tree_nd(dm, ta) : 0;
+    int ndb = tb >= 0 ? tree_nd(dm, tb) : 0;
+    const T* p = cr + CR_POS;
+    T* J = cr + CR_J;
+    for (int blk = 0; blk < 2; blk++) {
+      int t = blk == 0 ? ta : tb;
+      if (t < 0) continue;
+      int nd = blk == 0 ? nda : ndb;
+      int col0 = blk == 0 ? 0 : nda;
+      for (int j = 0; j < nd; j++) {
+        T col[3] = {0, 0, 0};
+        if (tr2 == t) {
+          T c2v[3];
+          body_jac_col(M, w, kb2, j, p, c2v);
+          for (int k = 0; k < 3; k++) col[k] += c2v[k];
+        }
+        if (tr1 == t) {
+          T c1v[3];
+          body_jac_col(M, w, kb1, j, p, c1v);
+          for (int k = 0; k < 3; k++) col[k] -= c1v[k];
+        }
+        for (int r = 0; r < 3; r++) J[r * CJ + col0 + j] = dot3(f + 3 * r, col);
+      }
+    }
+    ci[1] = ta;
+    ci[2] = tb;
+    ci[3] = pidx | (armflag << 16) | (nda << 20) | (ndb << 24);
+    // parameters
+    const T* prm = M.param + 8 * pidx;
+    T mu = prm[0];
+    T dist = cr[CR_DIST];
+    T imp = impedance(prm + 3, dist);
+    T Kk, Bb;
+    kb_params(M.dt, prm + 1, prm + 3, Kk, Bb);
+    auto invw_t = [&](int kb) -> T {
+      if (kb == 0) return T(0);
+      if (kb == 1) return M.belt_invw_t;
+      if (kb < 2 + K) return T(1) / M.cube[((size_t)arena * K + kb - 2) * 4 + 1];
+      return M.body[32 * ((kb - 2 - K) % 10) + 28];
+    };
+    T tran = invw_t(kb1) + invw_t(kb2);
+    T diag = tran + mu * mu * tran;
+    T R = (T(1) - imp) * diag / imp;
+    R = R > T(1e-15) ? R : T(1e-15);
+    cr[CR_MU] = mu;
+    cr[CR_D] = T(1) / R;
+    cr[CR_KD] = Kk * imp * dist;
+    cr[CR_BD] = Bb;
+    // efc velocity in the contact frame
+    for (int r = 0; r < 3; r++) {
+      T s = 0;
+      for (int j = 0; j < nda; j++) s += J[r * CJ + j] * v[tree_dof(dm, ta) + j];
+      for (int j = 0; j < ndb; j++) s += J[r * CJ + nda + j] * v[tree_dof(dm, tb) + j];
+      cr[CR_VEL + r] = s;
+    }
+  }
+  // ---- generic rows: gripper joint equality + active joint limits (lane 0)
+  if (LANE == 0) {
+    int nr = 0;
+    const T eq_sr[2] = {T(0.002), T(1.0)}, eq_si[5] = {T(0.98), T(0.9999), T(0.001), T(0.5), T(2.0)};
+    const T lim_sr[2] = {T(0.02), T(1.0)}, lim_si[5] = {T(0.9), T(0.95), T(0.001), T(0.5), T(2.0)};
+    for (int arm = 0; arm < A; arm++) {
+      int qa = 1 + 7 * K + 9 * arm, va = 1 + 6 * K + 9 * arm;
+      auto add = [&](int d0, T c0, int d1, T c1, T pos, T diag, const T* sr, const T* si) {
+        if (nr >= dm.maxrow) return;
+        int* ri = w.ri() + 4 * nr;
+        T* rr = w.rr() + RR_N * nr;
+        ri[0] = d0;
+        ri[1] = d1;
+        ri[2] = d1 >= 0 ? 0 : 1;  // 0 equality, 1 inequality
+        rr[RR_C0] = c0;
+        rr[RR_C1] = c1;
+        rr[RR_POS] = pos;
+        T imp = impedance(si, pos);
+        T Kk, Bb;
+        kb_params(M.dt, sr, si, Kk, Bb);
+        T R = (T(1) - imp) * diag / imp;
+        R = R > T(1e-15) ? R : T(1e-15);
+        rr[RR_D] = T(1) / R;
+        T vel = c0 * v[d0] + (d1 >= 0 ? c1 * v[d1] : T(0));
+        rr[RR_AREF] = -Bb * vel - Kk * imp * pos;
+        nr++;
+      };
+      add(va + 7, T(1), va + 8, T(-1), q[qa + 7] - q[qa + 8], M.dof[4 * 7 + 2] + M.dof[4 * 8 + 2], eq_sr, eq_si);
+      for (int d = 0; d < 9; d++) {
+        T lo = M.dof[4 * d], hi = M.dof[4 * d + 1];
+        T dl = q[qa + d] - lo, dh = hi - q[qa + d];
+        if (dl < T(0)) add(va + d, T(1), -1, T(0), dl, M.dof[4 * d + 2], lim_sr, lim_si);
+        if (dh < T(0)) add(va + d, T(-1), -1, T(0), dh, M.dof[4 * d + 2], lim_sr, lim_si);
+      }
+    }
+    misc[MISC_NROW] = nr;
+  }
+  SYNC();
+  // ---- tree -> contact masks
+  for (int t = LANE; t < dm.ntree; t += WAVE) {
+    uint64_t mk = 0;
+    for (int c = 0; c < ncon; c++) {
+      const int* ci = w.ci() + 4 * c;
+      if (ci[1] == t || ci[2] == t) mk |= 1ull << c;
+    }
+    w.tmask()[t] = mk;
+  }
+  (void)nv;
+  SYNC();
+}
+
+// ------------------------------------------------------------------------------------------------
+// block-diagonal M products and solves (belt scalar, cubes diagonal, arm 9x9 blocks)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ T Mdiag(const Model<T>& M, int arena, int i) {
+  const Dims& dm = M.dm;
+  if (i == 0) return M.belt_mass;
+  int k = (i - 1) / 6, r = (i - 1) % 6;
+  const T* c = M.cube + ((size_t)arena * dm.K + k) * 4;
+  return r < 3 ? c[1] : c[2];
+}
+
+// out = M x   (lanes over dofs)
+template <typename T>
+__device__ void mmul(const Model<T>& M, const Ws<T>& w, int arena, const T* x, T* out) {
+  const Dims& dm = M.dm;
+  int a0 = 1 + 6 * dm.K;
+  for (int i = LANE; i < dm.nv; i += WAVE) {
+    if (i < a0) {
+      out[i] = Mdiag(M, arena, i) * x[i];
+    } else {
+      int arm = (i - a0) / 9, r = (i - a0) % 9;
+      const T* Mb = w.Marm() + 81 * arm + 9 * r;
+      const T* xa = x + a0 + 9 * arm;
+      T s = 0;
+      for (int j = 0; j < 9; j++) s += Mb[j] * xa[j];
+      out[i] = s;
+    }
+  }
+}
+
+// in-place 9x9 Cholesky (lower), one lane
+template <typename T>
+__device__ void chol9(T* A) {
+  for (int j = 0; j < 9; j++) {
+    T s = A[9 * j + j];
+    for (int k = 0; k < j; k++) s -= A[9 * j + k] * A[9 * j + k];
+    T l = sqrt(s > T(1e-300) ? s : T(1e-300));
+    A[9 * j + j] = l;
+    for (int i = j + 1; i < 9; i++) {
+      T t = A[9 * i + j];
+      for (int k = 0; k < j; k++) t -= A[9 * i + k] * A[9 * j + k];
+      A[9 * i + j] = t / l;
+    }
+  }
+}
+template <typename T>
+__device__ void cholsolve9(const T* L, T* x) {
+  for (int i = 0; i < 9; i++) {
+    T t = x[i];
+    for (int k = 0; k < i; k++) t -= L[9 * i + k] * x[k];
+    x[i] = t / L[9 * i + i];
+  }
+  for (int i = 8; i >= 0; i--) {
+    T t = x[i];
+    for (int k = i + 1; k < 9; k++) t -= L[9 * k + i] * x[k];
+    x[i] = t / L[9 * i + i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Newton solver on the primal cost (see oracle/solver.c for the definition)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T edge_val(const T* x3, T mu, int e) {
+  return x3[0] + ((e & 1) ? -mu : mu) * x3[1 + (e >> 1)];
+}
+
+// evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
+template <typename T>
+__device__ T rows_eval(const Model<T>& M, const Ws<T>& w, const T* x, int ncon, int nrow) {
+  const Dims& dm = M.dm;
+  T cst = 0;
+  for (int c = LANE; c < ncon; c += WAVE) {
+    const int* ci = w.ci() + 4 * c;
+    T* cr = w.cr() + CR_N * c;
+    int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+    const T* J = cr + CR_J;
+    for (int r = 0; r < 3; r++) {
+      T s = 0;
+      if (ta >= 0) {
+        int o = tree_dof(dm, ta);
+        for (int j = 0; j < nda; j++) s += J[r * CJ + j] * x[o + j];
+      }
+      if (tb >= 0) {
+        int o = tree_dof(dm, tb);
+        for (int j = 0; j < ndb; j++) s += J[r * CJ + nda + j] * x[o + j];
+      }
+      cr[CR_JA + r] = s;
+    }
+    T mu = cr[CR_MU], D = cr[CR_D];
+    for (int e = 0; e < 4; e++) {
+      T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+      T jar = edge_val(cr + CR_JA, mu, e) - aref;
+      if (jar < T(0)) cst += T(0.5) * D * jar * jar;
+    }
+  }
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    T* rr = w.rr() + RR_N * r;
+    T jar = rr[RR_C0] * x[ri[0]] + (ri[1] >= 0 ? rr[RR_C1] * x[ri[1]] : T(0)) - rr[RR_AREF];
+    rr[RR_JAR] = jar;
+    if (ri[2] == 0 || jar < T(0)) cst += T(0.5) * rr[RR_D] * jar * jar;
+  }
+  return wave_sum(cst);
+}
+
+// f3 (per contact, stored in CR_F[0..2]) = D * sum_active jar_e c_e ; used for gradient / forces
+template <typename T>
+__device__ void contact_f3(const Ws<T>& w, int ncon) {
+  for (int c = LANE; c < ncon; c += WAVE) {
+    T* cr = w.cr() + CR_N * c;
+    T mu = cr[CR_MU], D = cr[CR_D];
+    T f0 = 0, f1 = 0, f2 = 0;
+    for (int e = 0; e < 4; e++) {
+      T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+      T jar = edge_val(cr + CR_JA, mu, e) - aref;
+      if (jar < T(0)) {
+        T s = D * jar;
+        f0 += s;
+        if (e < 2)
+          f1 += ((e & 1) ? -mu : mu) * s;
+        else
+          f2 += ((e & 1) ? -mu : mu) * s;
+      }
+      cr[CR_F + e] = jar < T(0) ? -D * jar : T(0);
+    }
+    cr[CR_JD + 0] = f0;  // temporarily hold f3 in the JD slots (overwritten by the line search)
+    cr[CR_JD + 1] = f1;
+    cr[CR_JD + 2] = f2;
+  }
+}
+
+// out_i = sum over rows of J_ri * (D jar)_r for active rows  (constraint part of the gradient)
+template <typename T>
+__device__ void gather_JtF(const Model<T>& M, const Ws<T>& w, int ncon, int nrow, T* out, bool add) {
+  const Dims& dm = M.dm;
+  for (int i = LANE; i < dm.nv; i += WAVE) {
+    int t = dof_tree(dm, i);
+    int jl = i - tree_dof(dm, t);
+    uint64_t mk = w.tmask()[t];
+    T s = 0;
+    while (mk) {
+      int c = __ffsll((unsigned long long)mk) - 1;
+      mk &= mk - 1;
+      const int* ci = w.ci() + 4 * c;
+      const T* cr = w.cr() + CR_N * c;
+      int nda = (ci[3] >> 20) & 15;
+      int col = ci[1] == t ? jl : nda + jl;
+      const T* J = cr + CR_J;
+      s += J[col] * cr[CR_JD] + J[CJ + col] * cr[CR_JD + 1] + J[2 * CJ + col] * cr[CR_JD + 2];
+    }
+    for (int r = 0; r < nrow; r++) {
+      const int* ri = w.ri() + 4 * r;
+      const T* rr = w.rr() + RR_N * r;
+      T jar = rr[RR_JAR];
+      if (!(ri[2] == 0 || jar < T(0))) continue;
+      T fr = rr[RR_D] * jar;
+      if (ri[0] == i) s += rr[RR_C0] * fr;
+      if (ri[1] == i) s += rr[RR_C1] * fr;
+    }
+    out[i] = add ? out[i] + s : s;
+  }
+}
+
+template <typename T>
+__device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
+  const Dims& dm = M.dm;
+  const int nv = dm.nv;
+  const int ncon = w.misc()[MISC_NCON], nrow = w.misc()[MISC_NROW];
+  T* a = w.a();
+  T* as = w.as();
+  T* g = w.g();
+  T* dir = w.dir();
+  T* Ma = w.Ma();
+  T* tmp = w.tmp();
+  T* H = w.H();
+  const T scale = T(1) / (M.meaninertia[arena] * T(nv > 1 ? nv : 1));
+  const T tol = (T)M.solver_tol;
+  // quadratic part helper: returns 1/2 (x-as)' M (x-as), leaves M(x-as) in Ma
+  auto quad = [&](const T* x) -> T {
+    for (int i = LANE; i < nv; i += WAVE) tmp[i] = x[i] - as[i];
+    SYNC();
+    mmul(M, w, arena, tmp, Ma);
+    SYNC();
+    T s = 0;
+    for (int i = LANE; i < nv; i += WAVE) s += T(0.5) * tmp[i] * Ma[i];
+    return wave_sum(s);
+  };
+  // warmstart: the cheaper of qacc_warmstart and qacc_smooth
+  T c_ws = quad(a) + rows_eval(M, w, a, ncon, nrow);
+  SYNC();
+  T c_sm = quad(as) + rows_eval(M, w, as, ncon, nrow);
+  SYNC();
+  if (!(c_ws < c_sm)) {
+    for (int i = LANE; i < nv; i += WAVE) a[i] = as[i];
+  }
+  SYNC();
+  T cost = quad(a) + rows_eval(M, w, a, ncon, nrow);
+  SYNC();
+  int it;
+  const int maxit = M.solver_iter;
+  const int ntri = nv * (nv + 1) / 2;
+  for (it = 0; it < maxit; it++) {
+    // gradient g = M(a - as) + J' D jar (active)
+    contact_f3(w, ncon);
+    SYNC();
+    gather_JtF(M, w, ncon, nrow, g, false);
+    SYNC();
+    T gn = 0;
+    for (int i = LANE; i < nv; i += WAVE) {
+      g[i] += Ma[i];
+      gn += g[i] * g[i];
+    }
+    gn = wave_sum(gn);
+    if (scale * sqrt(gn) < tol) break;
+    // Hessian H = M + sum_c B_c' K_c B_c + generic rows
+    for (int e = LANE; e < nv * nv; e += WAVE) H[e] = T(0);
+    SYNC();
+    {
+      int a0 = 1 + 6 * dm.K;
+      for (int i = LANE; i < nv; i += WAVE) {
+        if (i < a0) {
+          H[i * nv + i] = Mdiag(M, arena, i);
+        } else {
+          int arm = (i - a0) / 9, r = (i - a0) % 9;
+          for (int j = 0; j < 9; j++) H[i * nv + a0 + 9 * arm + j] = w.Marm()[81 * arm + 9 * r + j];
+        }
+      }
+    }
+    SYNC();
+    for (int c = 0; c < ncon; c++) {
+      const int* ci = w.ci() + 4 * c;
+      const T* cr = w.cr() + CR_N * c;
+      T mu = cr[CR_MU], D = cr[CR_D];
+      T Kc[6] = {0, 0, 0, 0, 0, 0};  // 00 11 22 01 02 12
+      bool any = false;
+      for (int e = 0; e < 4; e++) {
+        T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+        T jar = edge_val(cr + CR_JA, mu, e) - aref;
+        if (jar < T(0)) {
+          any = true;
+          T sg = (e & 1) ? -mu : mu;
+          Kc[0] += D;
+          if (e < 2) {
+            Kc[1] += D * sg * sg;
+            Kc[3] += D * sg;
+          } else {
+            Kc[2] += D * sg * sg;
+            Kc[4] += D * sg;
+          }
+        }
+      }
+      if (!any) continue;
+      int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+      int ncol = nda + ndb;
+      int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+      const T* J = cr + CR_J;
+      for (int e = LANE; e < ncol * ncol; e += WAVE) {
+        int ii = e / ncol, jj = e % ncol;
+        T b0 = J[ii], b1 = J[CJ + ii], b2 = J[2 * CJ + ii];
+        T k0 = Kc[0] * J[jj] + Kc[3] * J[CJ + jj] + Kc[4] * J[2 * CJ + jj];
+        T k1 = Kc[3] * J[jj] + Kc[1] * J[CJ + jj] + Kc[5] * J[2 * CJ + jj];
+        T k2 = Kc[4] * J[jj] + Kc[5] * J[CJ + jj] + Kc[2] * J[2 * CJ + jj];
+        int gi = ii < nda ? oa + ii : ob + ii - nda;
+        int gj = jj < nda ? oa + jj : ob + jj - nda;
+        H[gi * nv + gj] += b0 * k0 + b1 * k1 + b2 * k2;
+      }
+      SYNC();
+    }
+    if (LANE == 0) {
+      for (int r = 0; r < nrow; r++) {
+        const int* ri = w.ri() + 4 * r;
+        const T* rr = w.rr() + RR_N * r;
+        if (!(ri[2] == 0 || rr[RR_JAR] < T(0))) continue;
+        T D = rr[RR_D];
+        int d0 = ri[0], d1 = ri[1];
+        H[d0 * nv + d0] += D * rr[RR_C0] * rr[RR_C0];
+        if (d1 >= 0) {
+          H[d1 * nv + d1] += D * rr[RR_C1] * rr[RR_C1];
+          H[d0 * nv + d1] += D * rr[RR_C0] * rr[RR_C1];
+          H[d1 * nv + d0] += D * rr[RR_C0] * rr[RR_C1];
+        }
+      }
+    }
+    SYNC();
+    // dense Cholesky (right-looking over the column-major lower-triangle table)
+    int colstart = 0;
+    for (int k = 0; k < nv; k++) {
+      if (LANE == 0) {
+        T s = H[k * nv + k];
+        H[k * nv + k] = sqrt(s > T(1e-300) ? s : T(1e-300));
+      }
+      SYNC();
+      T lkk = H[k * nv + k];
+      for (int i = k + 1 + LANE; i < nv; i += WAVE) H[i * nv + k] /= lkk;
+      SYNC();
+      colstart += nv - k;  // start of column k+1 in the table
+      for (int e = colstart + LANE; e < ntri; e += WAVE) {
+        uint32_t ij = M.tri[e];
+        int i = ij & 0xFFFF, j = ij >> 16;
+        H[i * nv + j] -= H[i * nv + k] * H[j * nv + k];
+      }
+      SYNC();
+    }
+    // dir = -H^-1 g  (column-oriented substitutions)
+    for (int i = LANE; i < nv; i += WAVE) dir[i] = -g[i];
+    SYNC();
+    for (int k = 0; k < nv; k++) {
+      T xk = dir[k] / H[k * nv + k];
+      SYNC();
+      if (LANE == 0) dir[k] = xk;
+      for (int i = k + 1 + LANE; i < nv; i += WAVE) dir[i] -= H[i * nv + k] * xk;
+      SYNC();
+    }
+    for (int k = nv - 1; k >= 0; k--) {
+      T xk = dir[k] / H[k * nv + k];
+      SYNC();
+      if (LANE == 0) dir[k] = xk;
+      for (int i = LANE; i < k; i += WAVE) dir[i] -= H[k * nv + i] * xk;
+      SYNC();
+    }
+    // exact line search along dir (segment walking over the breakpoints of the inequality rows)
+    // Jd per contact (frame components) and per generic row
+    for (int c = LANE; c < ncon; c += WAVE) {
+      const int* ci = w.ci() + 4 * c;
+      T* cr = w.cr() + CR_N * c;
+      int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+      const T* J = cr + CR_J;
+      for (int r = 0; r < 3; r++) {
+        T s = 0;
+        if (ta >= 0) {
+          int o = tree_dof(dm, ta);
+          for (int j = 0; j < nda; j++) s += J[r * CJ + j] * dir[o + j];
+        }
+        if (tb >= 0) {
+          int o = tree_dof(dm, tb);
+          for (int j = 0; j < ndb; j++) s += J[r * CJ + nda + j] * dir[o + j];
+        }
+        cr[CR_JD + r] = s;
+      }
+    }
+    for (int r = LANE; r < nrow; r += WAVE) {
+      const int* ri = w.ri() + 4 * r;
+      T* rr = w.rr() + RR_N * r;
+      rr[RR_JD] = rr[RR_C0] * dir[ri[0]] + (ri[1] >= 0 ? rr[RR_C1] * dir[ri[1]] : T(0));
+    }
+    mmul(M, w, arena, dir, tmp);
+    SYNC();
+    T dMd = 0, dMa = 0;
+    for (int i = LANE; i < nv; i += WAVE) {
+      dMd += dir[i] * tmp[i];
+      dMa += dir[i] * Ma[i];
+    }
+    dMd = wave_sum(dMd);
+    dMa = wave_sum(dMa);
+    T alpha = 0;
+    for (int ls = 0; ls < 4 * (4 * ncon + nrow) + 4; ls++) {
+      T c0 = 0, c1 = 0, tn = T(3.0e38);
+      for (int c = LANE; c < ncon; c += WAVE) {
+        const T* cr = w.cr() + CR_N * c;
+        T mu = cr[CR_MU], D = cr[CR_D];
+        for (int e = 0; e < 4; e++) {
+          T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+          T jar = edge_val(cr + CR_JA, mu, e) - aref;
+          T jd = edge_val(cr + CR_JD, mu, e);
+          bool act;
+          if (jd != T(0)) {
+            T te = -jar / jd;
+            if (jd < T(0)) {
+              act = te <= alpha;
+            } else {
+              act = alpha < te;
+            }
+            if (te > alpha && te < tn) tn = te;
+          } else {
+            act = jar < T(0);
+          }
+          if (act) {
+            c0 += D * (jar + alpha * jd) * jd;
+            c1 += D * jd * jd;
+          }
+        }
+      }
+      for (int r = LANE; r < nrow; r += WAVE) {
+        const int* ri = w.ri() + 4 * r;
+        const T* rr = w.rr() + RR_N * r;
+        T jar = rr[RR_JAR], jd = rr[RR_JD], D = rr[RR_D];
+        bool act;
+        if (ri[2] == 0) {
+          act = true;
+        } else if (jd != T(0)) {
+          T te = -jar / jd;
+          act = jd < T(0) ? te <= alpha : alpha < te;
+          if (te > alpha && te < tn) tn = te;
+        } else {
+          act = jar < T(0);
+        }
+        if (act) {
+          c0 += D * (jar + alpha * jd) * jd;
+          c1 += D * jd * jd;
+        }
+      }
+      c0 = wave_sum(c0) + dMa + alpha * dMd;
+      c1 = wave_sum(c1) + dMd;
+      tn = wave_min(tn);
+      if (c0 >= T(0)) break;
+      T astar = alpha - c0 / c1;
+      if (astar <= tn) {
+        alpha = astar;
+        break;
+      }
+      alpha = tn;
+    }
+    for (int i = LANE; i < nv; i += WAVE) a[i] += alpha * dir[i];
+    SYNC();
+    T newcost = quad(a) + rows_eval(M, w, a, ncon, nrow);
+    SYNC();
+    T improvement = scale * (cost - newcost);
+    cost = newcost;
+    if (improvement < tol) {
+      it++;
+      break;
+    }
+  }
+  if (it >= maxit && LANE == 0) ctr[2] += 1;
+  if (LANE == 0) ctr[1] += it;
+  // final constraint forces at a
+  contact_f3(w, ncon);
+  SYNC();
+  gather_JtF(M, w, ncon, nrow, w.fc(), false);
+  SYNC();
+  for (int i = LANE; i < nv; i += WAVE) w.fc()[i] = -w.fc()[i];
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    T* rr = w.rr() + RR_N * r;
+    rr[RR_F] = (ri[2] == 0 || rr[RR_JAR] < T(0)) ? -rr[RR_D] * rr[RR_JAR] : T(0);
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------------------------------------
+// step2: actuation, smooth acceleration, constraint solve, implicitfast integration
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ void smooth_acc(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
+  const Dims& dm = M.dm;
+  const int K = dm.K, nv = dm.nv;
+  T* fa = w.fa();
+  for (int i = LANE; i < nv; i += WAVE) fa[i] = T(0);
+  SYNC();
+  if (actuation) {
+    for (int u = LANE; u < dm.nu; u += WAVE) {
+      T c = (T)w.ctrl()[u];
+      T lo = M.ctrlrange[2 * u], hi = M.ctrlrange[2 * u + 1];
+      c = c < lo ? lo : (c > hi ? hi : c);
+      T L = w.alen()[u], V = w.avel()[u];
+      if (u == 0) {
+        T f = M.belt_kv * c - M.belt_kv * V;
+        w.aforce()[u] = f;
+        fa[0] = f;
+      } else {
+        int arm = (u - 1) / 8, j = (u - 1) % 8;
+        int va = 1 + 6 * K + 9 * arm;
+        if (j < 7) {
+          T f = T(2000) * c + T(-2000) * L + T(-200) * V;
+          w.aforce()[u] = f;
+          fa[va + j] = f;
+        } else {
+          T f = T(100) * c + T(-100) * L + T(-10) * V;
+          f = f < T(-100) ? T(-100) : (f > T(100) ? T(100) : f);
+          w.aforce()[u] = f;
+          fa[va + 7] = T(0.5) * f;
+          fa[va + 8] = T(0.5) * f;
+        }
+      }
+    }
+  }
+  SYNC();
+  for (int i = LANE; i < nv; i += WAVE) w.fs()[i] = w.pb()[i] + fa[i];
+  SYNC();
+  // qacc_smooth = M^-1 qfrc_smooth
+  int a0 = 1 + 6 * K;
+  for (int i = LANE; i < a0; i += WAVE) w.as()[i] = w.fs()[i] / Mdiag(M, arena, i);
+  if (LANE < dm.A) {
+    T* L = w.Larm() + 81 * LANE;
+    for (int k = 0; k < 81; k++) L[k] = w.Marm()[81 * LANE + k];
+    chol9(L);
+    T x[9];
+    for (int k = 0; k < 9; k++) x[k] = w.fs()[a0 + 9 * LANE + k];
+    cholsolve9(L, x);
+    for (int k = 0; k < 9; k++) w.as()[a0 + 9 * LANE + k] = x[k];
+  }
+  SYNC();
+}
+
+template <typename T>
+__device__ void implicit_integrate(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
+  const Dims& dm = M.dm;
+  const int K = dm.K, nv = dm.nv;
+  const T dt = M.dt;
+  T* q = w.q();
+  T* v = w.v();
+  T* acc = w.tmp();
+  int a0 = 1 + 6 * K;
+  // belt: M + dt*(kv + damping); cubes: M
+  if (LANE == 0) {
+    T mb = M.belt_mass + dt * M.belt_damp + (actuation ? dt * M.belt_kv : T(0));
+    acc[0] = (w.fs()[0] + w.fc()[0]) / mb;
+  }
+  for (int i = 1 + LANE; i < a0; i += WAVE) acc[i] = (w.fs()[i] + w.fc()[i]) / Mdiag(M, arena, i);
+  if (LANE < dm.A) {
+    T* L = w.LBarm() + 81 * LANE;
+    for (int k = 0; k < 81; k++) L[k] = w.Marm()[81 * LANE + k];
+    if (actuation) {
+      for (int j = 0; j < 7; j++) L[9 * j + j] += dt * T(200);
+      T fg = w.aforce()[1 + 8 * LANE + 7];
+      if (fg > T(-100) && fg < T(100)) {
+        T d = dt * T(10) * T(0.25);
+        L[9 * 7 + 7] += d;
+        L[9 * 8 + 8] += d;
+        L[9 * 7 + 8] += d;
+        L[9 * 8 + 7] += d;
+      }
+    }
+    chol9(L);
+    T x[9];
+    for (int k = 0; k < 9; k++) x[k] = w.fs()[a0 + 9 * LANE + k] + w.fc()[a0 + 9 * LANE + k];
+    cholsolve9(L, x);
+    for (int k = 0; k < 9; k++) acc[a0 + 9 * LANE + k] = x[k];
+  }
+  SYNC();
+  for (int i = LANE; i < nv; i += WAVE) v[i] += dt * acc[i];
+  SYNC();
+  // positions with the new velocities (mj_integratePos)
+  if (LANE == 0) q[0] += dt * v[0];
+  for (int k = LANE; k < K; k += WAVE) {
+    T* qq = q + 1 + 7 * k;
+    const T* vv = v + 1 + 6 * k;
+    for (int c = 0; c < 3; c++) qq[c] += dt * vv[c];
+    T ax[3] = {vv[3], vv[4], vv[5]};
+    T nrm = sqrt(dot3(ax, ax));
+    if (nrm < T(1e-15)) {
+      ax[0] = 1;
+      ax[1] = ax[2] = 0;
+    } else {
+      for (int c = 0; c < 3; c++) ax[c] /= nrm;
+    }
+    T ang = dt * nrm;
+    T qr[4];
+    if (ang == T(0)) {
+      qr[0] = 1;
+      qr[1] = qr[2] = qr[3] = 0;
+    } else {
+      T s = sin(ang * T(0.5));
+      qr[0] = cos(ang * T(0.5));
+      qr[1] = ax[0] * s;
+      qr[2] = ax[1] * s;
+      qr[3] = ax[2] * s;
+    }
+    T qu[4] = {qq[3], qq[4], qq[5], qq[6]};
+    T n = sqrt(qu[0] * qu[0] + qu[1] * qu[1] + qu[2] * qu[2] + qu[3] * qu[3]);
+    if (n < T(1e-15)) {
+      qu[0] = 1;
+      qu[1] = qu[2] = qu[3] = 0;
+    } else if (fabs(n - T(1)) > T(1e-15)) {
+      for (int c = 0; c < 4; c++) qu[c] /= n;
+    }
+    qq[3] = qu[0] * qr[0] - qu[1] * qr[1] - qu[2] * qr[2] - qu[3] * qr[3];
+    qq[4] = qu[0] * qr[1] + qu[1] * qr[0] + qu[2] * qr[3] - qu[3] * qr[2];
+    qq[5] = qu[0] * qr[2] - qu[1] * qr[3] + qu[2] * qr[0] + qu[3] * qr[1];
+    qq[6] = qu[0] * qr[3] + qu[1] * qr[2] - qu[2] * qr[1] + qu[3] * qr[0];
+  }
+  int qa0 = 1 + 7 * K;
+  for (int i = LANE; i < 9 * dm.A; i += WAVE) q[qa0 + i] += dt * v[a0 + i];
+  SYNC();
+}
+
+// ------------------------------------------------------------------------------------------------
+// task layer (lane 0 unless noted; float64 like the reference's Python)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t pcg_next(uint64_t* st) {
+  const uint64_t MH = 0x2360ED051FC65DA4ULL, ML = 0x4385DF649FCCF645ULL;
+  uint64_t sh = st[0], sl = st[1];
+  uint64_t lo = sl * ML;
+  uint64_t hi = __umul64hi(sl, ML) + sl * MH + sh * ML;
+  uint64_t lo2 = lo + st[3];
+  uint64_t carry = lo2 < lo ? 1ull : 0ull;
+  uint64_t hi2 = hi + st[2] + carry;
+  st[0] = hi2;
+  st[1] = lo2;
+  uint64_t x = hi2 ^ lo2;
+  unsigned rot = (unsigned)(hi2 >> 58);
+  return (x >> rot) | (x << ((-rot) & 63));
+}
+__device__ __forceinline__ double pcg_double(uint64_t* st) {
+  return (double)(pcg_next(st) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+template <typename T>
+__device__ void hide_cube(const Dims& dm, T* q, T* v, int32_t* ti, int obj) {
+  ti[dm.K + ti[2 * dm.K + I_NOUT]] = obj;
+  ti[2 * dm.K + I_NOUT]++;
+  T* qq = q + 1 + 7 * obj;
+  qq[0] = T(4.0 + 1.0);
+  qq[1] = T(ti[2 * dm.K + I_HIDDEN] * 0.2);
+  qq[2] = T(1.0);
+  qq[3] = T(1.0);
+  qq[4] = qq[5] = qq[6] = T(0);
+  T* vv = v + 1 + 6 * obj;
+  for (int k = 0; k < 6; k++) vv[k] = T(0);
+  ti[2 * dm.K + I_HIDDEN]++;
+}
+
+__device__ __forceinline__ void pop_at(int32_t* list, int32_t* n, int idx) {
+  for (int i = idx; i < *n - 1; i++) list[i] = list[i + 1];
+  (*n)--;
+  list[*n] = -1;
+}
+
+// TaskManager.reset (task_utils.py:146-156) + BaseEnv.reset_sim bits (base_env.py:184-190)
+template <typename T>
+__device__ void task_reset(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, double* ctrl) {
+  const Dims& dm = M.dm;
+  const int K = dm.K;
+  for (int k = 0; k < K; k++) {
+    T* qq = q + 1 + 7 * k;
+    qq[0] = T(4.0);
+    qq[1] = T(0.0 + k * 0.2);
+    qq[2] = T(1.0);
+    qq[3] = T(1.0);
+    qq[4] = qq[5] = qq[6] = T(0);
+    T* vv = v + 1 + 6 * k;
+    for (int c = 0; c < 6; c++) vv[c] = T(0);
+    ti[K + k] = k;
+    ti[k] = -1;
+  }
+  int32_t* ts = ti + 2 * K;
+  ts[I_NIN] = 0;
+  ts[I_NOUT] = K;
+  ts[I_STEP] = ts[I_SINCE] = ts[I_FAIL] = ts[I_HIDDEN] = 0;
+  ts[I_S0] = ts[I_S1] = 0;
+  ts[I_LS0] = ts[I_LS1] = 0;
+  for (int u = 0; u < dm.nu; u++) ctrl[u] = 0.0;
+  td[0] = M.spawn_freq0;  // spawn_freq
+  td[1] = M.init_speed;   // conveyor speed
+  td[2] = 0.0;            // play_time
+}
+
+template <typename T>
+__device__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr) {
+  const Dims& dm = M.dm;
+  const int K = dm.K;
+  int32_t* ins = ti;
+  int32_t* outs = ti + K;
+  int32_t* ts = ti + 2 * K;
+  int spawn_steps = (int)(1.0 / (0.1 * td[0]));
+  if (ts[I_STEP] == 0 || ts[I_SINCE] >= spawn_steps) {
+    if (ts[I_NOUT] > 0) {
+      int obj = outs[0];
+      pop_at(outs, &ts[I_NOUT], 0);
+      T* qq = q + 1 + 7 * obj;
+      qq[0] = T(0.0);
+      qq[1] = T(1.0);
+      qq[2] = T(2.0);
+      for (int k = 0; k < 4; k++) qq[3 + k] = T(0.0 + 1.0 * pcg_double(rng));
+      ins[ts[I_NIN]++] = obj;
+    }
+    ts[I_SINCE] = 0;
+  }
+  if (ts[I_NIN] > 0) {
+    int n = ts[I_NIN];
+    bool oob[64];
+    for (int i = 0; i < n; i++) {
+      const T* qq = q + 1 + 7 * ins[i];
+      double x = (double)qq[0], y = (double)qq[1], z = (double)qq[2];
+      oob[i] = fabs(x) > 1.2 || y < -1.5 || z < 0.9;
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      if (!oob[i]) continue;
+      int obj = ins[i];
+      pop_at(ins, &ts[I_NIN], i);
+      hide_cube(dm, q, v, ti, obj);
+      ts[I_FAIL]++;
+    }
+    if (ts[I_NIN] > 0) {
+      int n2 = ts[I_NIN];
+      double pos[64][3];
+      for (int i = 0; i < n2; i++)
+        for (int c = 0; c < 3; c++) pos[i][c] = (double)q[1 + 7 * ins[i] + c];
+      for (int b = 0; b < 2; b++) {
+        double bx = b == 0 ? M.bucket_x0 : M.bucket_x1, by = M.bucket_y, bz = M.bucket_z;
+        for (int i = n2 - 1; i >= 0; i--) {
+          bool in_x = fabs(pos[i][0] - bx) <= 0.6 * 0.29;
+          bool in_y = fabs(pos[i][1] - by) <= 0.6 * 0.29;
+          bool in_z = pos[i][2] - bz - 0.02 / 2 <= 0.07;
+          if (!(in_x && in_y && in_z)) continue;
+          if (i >= ts[I_NIN]) {  // reference: IndexError (task_utils.py:103-113 index reuse)
+            ctr[3] += 1;
+            continue;
+          }
+          int obj = ins[i];
+          pop_at(ins, &ts[I_NIN], i);
+          hide_cube(dm, q, v, ti, obj);
+          ts[b == 0 ? I_S0 : I_S1]++;
+        }
+      }
+    }
+  }
+  ts[I_STEP]++;
+  ts[I_SINCE]++;
+  return ts[I_FAIL] > 0;
+}
+
+// observation row (environments.py:55-82 over base_env.py:149-175): arms (q[8], qd[8], ctrl[8]) then
+// in-scene cubes sorted by x (stable), zero padded: poses K x 7, velocities K x 6
+template <typename T>
+__device__ void write_obs(const Model<T>& M, const Ws<T>& w, const int32_t* ti, float* obs) {
+  const Dims& dm = M.dm;
+  const int A = dm.A, K = dm.K;
+  const T* q = w.q();
+  const T* v = w.v();
+  int* idx = w.sortidx();
+  if (LANE == 0) {
+    int n = ti[2 * K + I_NIN];
+    for (int i = 0; i < n; i++) idx[i] = ti[i];
+    for (int i = 1; i < n; i++) {
+      int vi = idx[i];
+      T x = q[1 + 7 * vi];
+      int j = i - 1;
+      while (j >= 0 && q[1 + 7 * idx[j]] > x) {
+        idx[j + 1] = idx[j];
+        j--;
+      }
+      idx[j + 1] = vi;
+    }
+  }
+  SYNC();
+  int n = ti[2 * K + I_NIN];
+  for (int e = LANE; e < dm.obs_dim; e += WAVE) {
+    float val;
+    if (e < 24 * A) {
+      int arm = e / 24, r = e % 24;
+      if (r < 8)
+        val = (float)q[1 + 7 * K + 9 * arm + r];
+      else if (r < 16)
+        val = (float)v[1 + 6 * K + 9 * arm + r - 8];
+      else
+        val = (float)w.ctrl()[1 + 8 * arm + r - 16];
+    } else if (e < 24 * A + 7 * K) {
+      int k = (e - 24 * A) / 7, c = (e - 24 * A) % 7;
+      val = k < n ? (float)q[1 + 7 * idx[k] + c] : 0.0f;
+    } else {
+      int k = (e - 24 * A - 7 * K) / 6, c = (e - 24 * A - 7 * K) % 6;
+      val = k < n ? (float)v[1 + 6 * idx[k] + c] : 0.0f;
+    }
+    obs[e] = val;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena, bool stage_copy) {
+  const Dims& dm = M.dm;
+  const T* ph = S.phys + (size_t)arena * dm.phys_stride;
+  const T* src_q = ph + (stage_copy ? dm.nq + dm.nv : 0);
+  const T* src_v = ph + dm.nq + (stage_copy ? dm.nq + dm.nv : 0);
+  for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = src_q[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) w.v()[i] = src_v[i];
+}
+
+template <typename T>
+__device__ void init_static_geoms(const Model<T>& M, const Ws<T>& w) {
+  for (int g = LANE; g < M.dm.ngc; g += WAVE) {
+    const int* gi = M.geom_i + 4 * g;
+    if (gi[2] != 0) continue;
+    const T* gg = M.geom + 16 * g;
+    for (int c = 0; c < 3; c++) w.gx()[3 * g + c] = gg[c];
+    if (gi[3] >= 0)
+      for (int c = 0; c < 9; c++) w.gR()[9 * gi[3] + c] = gg[3 + c];
+  }
+}
+
+// physics.reset() + TaskManager.reset() + after_reset forward (actuation disabled) -> warmstart
+template <typename T>
+__device__ void arena_reset(const Model<T>& M, const Ws<T>& w, int arena, int32_t* ti, double* td, int64_t* ctr) {
+  const Dims& dm = M.dm;
+  T* q = w.q();
+  T* v = w.v();
+  for (int i = LANE; i < dm.nq; i += WAVE) q[i] = T(0);
+  for (int i = LANE; i < dm.nv; i += WAVE) {
+    v[i] = T(0);
+    w.a()[i] = T(0);
+  }
+  SYNC();
+  if (LANE == 0) task_reset(M, q, v, ti, td, w.ctrl());
+  SYNC();
+  stage(M, w, arena, ctr);
+  smooth_acc(M, w, arena, false);
+  if (w.misc()[MISC_NCON] + w.misc()[MISC_NROW] > 0) {
+    newton(M, w, arena, ctr);
+  } else {
+    for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = w.as()[i];
+    SYNC();
+  }
+}
+
+template <typename T>
+__device__ void store_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena) {
+  const Dims& dm = M.dm;
+  T* ph = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nq; i += WAVE) ph[i] = w.q()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[dm.nq + i] = w.v()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + 2 * dm.nv + i] = w.a()[i];
+  double* db = S.dbl + (size_t)arena * dm.dbl_stride;
+  for (int u = LANE; u < dm.nu; u += WAVE) db[u] = w.ctrl()[u];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L, float* obs, const uint8_t* mask) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int arena = blockIdx.x;
+  const Dims& dm = M.dm;
+  if (mask && !mask[arena]) return;
+  Ws<T> w{smem, &L};
+  int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
+  double* td = S.dbl + (size_t)arena * dm.dbl_stride + dm.nu;
+  int64_t* ctr = S.counters + 4 * (size_t)arena;
+  init_static_geoms(M, w);
+  SYNC();
+  arena_reset(M, w, arena, ti, td, ctr);
+  // stage state = reset state
+  T* ph = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nq; i += WAVE) ph[dm.nq + dm.nv + i] = w.q()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + dm.nv + i] = w.v()[i];
+  store_state(M, S, w, arena);
+  if (LANE == 0) {
+    td[2 * dm.A + 3] = 0.0;  // episode return
+    ti[2 * dm.K + I_EPLEN] = 0;
+  }
+  SYNC();
+  if (obs) write_obs(M, w, ti, obs + (size_t)arena * dm.obs_dim);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L, StepIO io) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int arena = blockIdx.x;
+  const Dims& dm = M.dm;
+  const int A = dm.A, K = dm.K, nu = dm.nu;
+  Ws<T> w{smem, &L};
+  int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
+  double* td = S.dbl + (size_t)arena * dm.dbl_stride + nu;  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
+  uint64_t* rng = S.rng + 4 * (size_t)arena;
+  int64_t* ctr = S.counters + 4 * (size_t)arena;
+  const float* act = io.actions + (size_t)arena * dm.act_dim;
+  // ---- ctrl_target (double) and the clipped AllFullRL control (environments.py:84-102, base_env.py:255-262)
+  double* ctrl = w.ctrl();
+  const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
+  for (int u = LANE; u < nu; u += WAVE) ctrl[u] = dsrc[u];
+  double speed = td[1];
+  double* uctl = w.uctl();
+  for (int u = LANE; u < nu; u += WAVE) {
+    double c;
+    if (u == 0) {
+      c = speed;
+    } else {
+      int j = (u - 1) % 8;
+      float a = (float)tanh((double)act[u - 1]);  // correctly rounded float32 tanh (np.tanh on float32)
+      float s = (a + 1.0f) * 0.5f;
+      double lo = (double)M.ctrlrange[2 * (1 + j)], hi = (double)M.ctrlrange[2 * (1 + j) + 1];
+      c = lo + (double)s * (hi - lo);
+    }
+    double lo = (double)M.ctrlrange[2 * u], hi = (double)M.ctrlrange[2 * u + 1];
+    uctl[u] = c < lo ? lo : (c > hi ? hi : c);
+  }
+  init_static_geoms(M, w);
+  // warmstart
+  const T* ph = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
+  SYNC();
+  // ---- stage at the state of the last mj_step1 (pre-teleport), then the current state
+  load_state(M, S, w, arena, true);
+  SYNC();
+  stage(M, w, arena, ctr);
+  load_state(M, S, w, arena, false);
+  SYNC();
+  const double lp = 0.001 / (0.001 + M.pt_time);
+  bool force_term = false;
+  for (int t = 0; t < dm.frame_skip; t++) {
+    for (int u = LANE; u < nu; u += WAVE) {
+      double ct = ctrl[u] + (uctl[u] - ctrl[u]) * lp;
+      ctrl[u] = u == 0 ? -speed : ct;
+    }
+    SYNC();
+    smooth_acc(M, w, arena, true);
+    if (w.misc()[MISC_NCON] + w.misc()[MISC_NROW] > 0) {
+      newton(M, w, arena, ctr);
+    } else {
+      for (int i = LANE; i < dm.nv; i += WAVE) {
+        w.a()[i] = w.as()[i];
+        w.fc()[i] = T(0);
+      }
+      SYNC();
+    }
+    implicit_integrate(M, w, arena, true);
+    if (t == dm.frame_skip - 1) {
+      // contact-force termination on the contacts + forces of the final solve
+      int ncon = w.misc()[MISC_NCON];
+      bool hit = false;
+      for (int c = LANE; c < ncon; c += WAVE) {
+        const int* ci = w.ci() + 4 * c;
+        if (!((ci[3] >> 16) & 1)) continue;
+        const T* cr = w.cr() + CR_N * c;
+        const T* f = cr + CR_F;
+        T fn = f[0] + f[1] + f[2] + f[3];
+        T f1 = (f[0] - f[1]) * cr[CR_MU], f2 = (f[2] - f[3]) * cr[CR_MU];
+        T mx = fabs(fn);
+        mx = fabs(f1) > mx ? fabs(f1) : mx;
+        mx = fabs(f2) > mx ? fabs(f2) : mx;
+        if ((double)mx > M.force_thr) hit = true;
+      }
+      force_term = __ballot(hit) != 0ull;
+    } else {
+      stage(M, w, arena, ctr);
+    }
+  }
+  // gripper sites at the final state (the last mj_step1's site_xpos)
+  if (LANE < A) arm_chain(M, w, LANE, false);
+  SYNC();
+  // stage state for the next env-step = state before the TaskManager's teleports
+  T* phw = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
+  double* sc = w.scal();  // [0] reward, [1] terminated, [2] out_of_reach
+  if (LANE == 0) {
+    int fail = task_step(M, w.q(), w.v(), ti, td, rng, ctr);
+    // BaseEnv.step_sim bookkeeping (base_env.py:266-270)
+    double dt_env = 0.001 * dm.frame_skip;
+    td[2] += dt_env;
+    td[1] += M.accel * dt_env;
+    td[0] *= M.spawn_inc;
+    int32_t* ts = ti + 2 * K;
+    int sd = (ts[I_S0] + ts[I_S1]) - (ts[I_LS0] + ts[I_LS1]);
+    double rew;
+    if (M.env_class == FM_ENV_FACTORY_SCORE) {
+      rew = sd;
+    } else {
+      double gc = 0, bc = 0;
+      int closest[16];
+      double* lg = td + 3;
+      double* lb = td + 3 + A;
+      for (int i = 0; i < A; i++) {
+        closest[i] = -1;
+        if (ts[I_NIN] == 0) continue;
+        const T* gp = w.site() + 3 * i;
+        double best = 0;
+        int bi = -1;
+        for (int c = 0; c < ts[I_NIN]; c++) {
+          const T* qq = w.q() + 1 + 7 * ti[c];
+          double dx = (double)qq[0] - (double)gp[0], dy = (double)qq[1] - (double)gp[1],
+                 dz = (double)qq[2] - (double)gp[2];
+          double dd = sqrt(dx * dx + dy * dy + dz * dz);
+          if (bi < 0 || dd < best) {
+            best = dd;
+            bi = c;
+          }
+        }
+        closest[i] = ti[bi];
+        gc += lg[i] - best;
+        lg[i] = best;
+      }
+      for (int i = 0; i < A; i++) {
+        if (closest[i] < 0) continue;
+        const T* qq = w.q() + 1 + 7 * closest[i];
+        double bx = (i % 2) == 0 ? M.bucket_x0 : M.bucket_x1;
+        double dx = (double)qq[0] - bx, dy = (double)qq[1] - M.bucket_y, dz = (double)qq[2] - M.bucket_z;
+        double dd = sqrt(dx * dx + dy * dy + dz * dz);
+        bc += lb[i] - dd;
+        lb[i] = dd;
+      }
+      float ss = 0.0f;
+      for (int i = 0; i < 8 * A; i++)
+        if (i % 8 != 7) ss += act[i] * act[i];
+      float an = expf(-sqrtf(ss));
+      double prog = M.base_reward + M.w_grip * gc + M.w_bucket * bc + M.w_action * (double)an;
+      rew = sd > 0 ? (double)sd : prog;
+    }
+    ts[I_LS0] = ts[I_S0];
+    ts[I_LS1] = ts[I_S1];
+    sc[0] = rew;
+    sc[1] = (fail || force_term) ? 1.0 : 0.0;
+    sc[2] = fail ? 1.0 : 0.0;
+    td[3 + 2 * A] += rew;  // Monitor episode return
+    ts[I_EPLEN]++;
+  }
+  SYNC();
+  const int term = sc[1] != 0.0;
+  const int s_fail = sc[2] != 0.0;
+  const double s_rew = sc[0];
+  if (LANE == 0) {
+    int32_t* ts = ti + 2 * K;
+    if (io.reward) io.reward[arena] = (float)s_rew;
+    if (io.terminated) io.terminated[arena] = (uint8_t)term;
+    if (io.truncated) io.truncated[arena] = 0;
+    if (io.scores) {
+      io.scores[2 * arena] = ts[I_S0];
+      io.scores[2 * arena + 1] = ts[I_S1];
+    }
+    if (io.num_obj) io.num_obj[arena] = ts[I_NIN];
+    if (io.play_time) io.play_time[arena] = td[2];
+    if (io.conveyor_speed) io.conveyor_speed[arena] = td[1];
+    if (io.out_of_reach) io.out_of_reach[arena] = (uint8_t)s_fail;
+    if (io.force_terminate) io.force_terminate[arena] = (uint8_t)force_term;
+    if (term) {
+      if (io.ep_return) io.ep_return[arena] = td[3 + 2 * A];
+      if (io.ep_len) io.ep_len[arena] = ts[I_EPLEN];
+      if (io.terminal_scores) {
+        io.terminal_scores[2 * arena] = ts[I_S0];
+        io.terminal_scores[2 * arena + 1] = ts[I_S1];
+      }
+    }
+  }
+  if (term) {
+    if (io.terminal_obs) write_obs(M, w, ti, io.terminal_obs + (size_t)arena * dm.obs_dim);
+    SYNC();
+    arena_reset(M, w, arena, ti, td, ctr);
+    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
+    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
+    if (LANE == 0) {
+      td[3 + 2 * A] = 0.0;
+      ti[2 * K + I_EPLEN] = 0;
+    }
+    SYNC();
+  }
+  store_state(M, S, w, arena);
+  if (io.obs) write_obs(M, w, ti, io.obs + (size_t)arena * dm.obs_dim);
+}
+
+
+// diagnostic: run one mj_step1 + acceleration stage on arena `arena` at its stored state and dump
+// internals (float64) for comparison with the oracle.  Layout (see fm_debug_dump in the C ABI):
+// [0] ncon [1] nrow | Marm A*81 | pb nv | as nv | a nv | fc nv | site 3A | bpos 30A | bcom 30A |
+// dax 27A | contacts 64 x (g1 g2 dist pos3 frame9 mu D) | rows 20A x (d0 d1 pos D aref f)
+template <typename T>
+__global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L, int arena, int actuated,
+                                                   double* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const Dims& dm = M.dm;
+  Ws<T> w{smem, &L};
+  int64_t* ctr = S.counters + 4 * (size_t)arena;
+  const T* ph = S.phys + (size_t)arena * dm.phys_stride;
+  const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
+  for (int u = LANE; u < dm.nu; u += WAVE) w.ctrl()[u] = dsrc[u];
+  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
+  init_static_geoms(M, w);
+  SYNC();
+  load_state(M, S, w, arena, true);
+  SYNC();
+  stage(M, w, arena, ctr);
+  smooth_acc(M, w, arena, actuated != 0);
+  if (w.misc()[MISC_NCON] + w.misc()[MISC_NROW] > 0) newton(M, w, arena, ctr);
+  SYNC();
+  const int A = dm.A, nv = dm.nv;
+  int ncon = w.misc()[MISC_NCON], nrow = w.misc()[MISC_NROW];
+  double* o = out;
+  if (LANE == 0) {
+    o[0] = ncon;
+    o[1] = nrow;
+  }
+  o += 2;
+  for (int i = LANE; i < 81 * A; i += WAVE) o[i] = (double)w.Marm()[i];
+  o += 81 * A;
+  for (int i = LANE; i < nv; i += WAVE) {
+    o[i] = (double)w.pb()[i];
+    o[nv + i] = (double)w.as()[i];
+    o[2 * nv + i] = (double)w.a()[i];
+    o[3 * nv + i] = (double)w.fc()[i];
+  }
+  o += 4 * nv;
+  for (int i = LANE; i < 3 * A; i += WAVE) o[i] = (double)w.site()[i];
+  o += 3 * A;
+  for (int i = LANE; i < 30 * A; i += WAVE) {
+    o[i] = (double)w.bpos()[i];
+    o[30 * A + i] = (double)w.bcom()[i];
+  }
+  o += 60 * A;
+  for (int i = LANE; i < 27 * A; i += WAVE) o[i] = (double)w.dax()[i];
+  o += 27 * A;
+  for (int c = LANE; c < 64; c += WAVE) {
+    double* r = o + 17 * c;
+    if (c < ncon) {
+      const int* ci = w.ci() + 4 * c;
+      const T* cr = w.cr() + CR_N * c;
+      r[0] = M.geom_i[4 * (ci[0] & 4095)];
+      r[1] = M.geom_i[4 * ((ci[0] >> 12) & 4095)];
+      r[2] = cr[CR_DIST];
+      for (int k = 0; k < 3; k++) r[3 + k] = cr[CR_POS + k];
+      for (int k = 0; k < 9; k++) r[6 + k] = cr[CR_FR + k];
+      r[15] = cr[CR_MU];
+      r[16] = cr[CR_D];
+    } else {
+      for (int k = 0; k < 17; k++) r[k] = 0;
+    }
+  }
+  o += 17 * 64;
+  for (int r = LANE; r < 20 * A; r += WAVE) {
+    double* x = o + 6 * r;
+    if (r < nrow) {
+      const int* ri = w.ri() + 4 * r;
+      const T* rr = w.rr() + RR_N * r;
+      x[0] = ri[0];
+      x[1] = ri[1];
+      x[2] = rr[RR_POS];
+      x[3] = rr[RR_D];
+      x[4] = rr[RR_AREF];
+      x[5] = rr[RR_F];
+    } else {
+      for (int k = 0; k < 6; k++) x[k] = 0;
+    }
+  }
+}
+
+}  // namespace fm
+
+// =================================================================================================
+// host side: handle, uploads, C ABI
+// =================================================================================================
+using namespace fm;
+
+static thread_local std::string g_err;
+
+static int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) return set_err(FM_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct fm_handle {
+  fm_config cfg;
+  SceneHost sc;
+  Dims dm;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  bool fp64 = false;
+  bool was_reset = false;
+  Lay lay;
+  std::vector<void*> allocs;
+  // device model arrays (typed by precision, stored as void*)
+  void* arm_base = nullptr;
+  void* body = nullptr;
+  void* dof = nullptr;
+  void* ctrlrange = nullptr;
+  void* geom = nullptr;
+  int* geom_i = nullptr;
+  uint32_t* pair = nullptr;
+  void* param = nullptr;
+  void* cube = nullptr;
+  void* meaninertia = nullptr;
+  uint32_t* tri = nullptr;
+  // state
+  void* phys = nullptr;
+  double* dbl = nullptr;
+  int32_t* ints = nullptr;
+  uint64_t* rng = nullptr;
+  int64_t* counters = nullptr;
+};
+
+template <typename T>
+static int upload(fm_handle* h, void** dst, const std::vector<double>& src) {
+  std::vector<T> tmp(src.size());
+  for (size_t i = 0; i < src.size(); i++) tmp[i] = (T)src[i];
+  size_t bytes = std::max<size_t>(tmp.size(), 1) * sizeof(T);
+  HIPCHK(hipMalloc(dst, bytes));
+  h->allocs.push_back(*dst);
+  if (!tmp.empty()) HIPCHK(hipMemcpy(*dst, tmp.data(), tmp.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+template <typename U>
+static int upload_raw(fm_handle* h, U** dst, const std::vector<U>& src) {
+  size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(U);
+  HIPCHK(hipMalloc((void**)dst, bytes));
+  h->allocs.push_back(*dst);
+  if (!src.empty()) HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(U), hipMemcpyHostToDevice));
+  return 0;
+}
+
+static Lay lds_layout(const Dims& d, int tsize) {
+  Lay L;
+  int off = 0;
+  auto take = [&](int bytes) {
+    int o = off;
+    off += (bytes + 15) & ~15;
+    return o;
+  };
+  int nv = d.nv, A = d.A, K = d.K;
+  L.q = take(tsize * d.nq);
+  L.v = take(tsize * nv);
+  L.a = take(tsize * nv);
+  L.as = take(tsize * nv);
+  L.fs = take(tsize * nv);
+  L.fc = take(tsize * nv);
+  L.pb = take(tsize * nv);
+  L.g = take(tsize * nv);
+  L.dir = take(tsize * nv);
+  L.Ma = take(tsize * nv);
+  L.tmp = take(tsize * nv);
+  L.fa = take(tsize * nv);
+  L.ctrl = take(8 * d.nu);
+  L.alen = take(tsize * d.nu);
+  L.avel = take(tsize * d.nu);
+  L.aforce = take(tsize * d.nu);
+  L.bpos = take(tsize * 30 * A);
+  L.bR = take(tsize * 90 * A);
+  L.bcom = take(tsize * 30 * A);
+  L.bIw = take(tsize * 60 * A);
+  L.bF = take(tsize * 30 * A);
+  L.bN = take(tsize * 30 * A);
+  L.dax = take(tsize * 27 * A);
+  L.danc = take(tsize * 27 * A);
+  L.site = take(tsize * 3 * A);
+  L.cR = take(tsize * 9 * K);
+  L.Marm = take(tsize * 81 * A);
+  L.Larm = take(tsize * 81 * A);
+  L.LBarm = take(tsize * 81 * A);
+  L.gx = take(tsize * 3 * d.ngc);
+  L.gR = take(tsize * 9 * d.nbox);
+  L.H = take(tsize * nv * nv);
+  L.c_i = take(4 * 4 * d.maxcon);
+  L.c_r = take(tsize * CR_N * d.maxcon);
+  L.r_i = take(4 * 4 * d.maxrow);
+  L.r_r = take(tsize * RR_N * d.maxrow);
+  L.surv = take(2 * MAXSURV);
+  L.tmask = take(8 * d.ntree);
+  L.misc = take(4 * 16);
+  L.sort = take(4 * K);
+  L.uctl = take(8 * d.nu);
+  L.scal = take(8 * 4);
+  L.total = off;
+  return L;
+}
+
+template <typename T>
+static Model<T> make_model(const fm_handle* h) {
+  Model<T> M;
+  M.dm = h->dm;
+  M.dt = T(0.001);
+  M.grav = T(9.81);
+  M.belt_mass = T(1000);
+  M.belt_kv = T(1e4);
+  M.belt_damp = T(5e-4);
+  M.belt_invw_t = T((1.0 / 1000.0) / 3.0);
+  const fm_config& c = h->cfg;
+  M.init_speed = c.initial_conveyor_speed;
+  M.accel = c.conveyor_acceleration;
+  M.pt_time = c.pt_time;
+  M.force_thr = c.force_contact_threshold;
+  M.spawn_freq0 = c.spawn_freq * h->dm.A;
+  M.spawn_inc = c.spawn_freq_increase;
+  M.w_grip = c.gripper_to_closest_cube_reward_factor;
+  M.w_bucket = c.closest_cube_to_bucket_reward_factor;
+  M.w_action = c.small_action_norm_reward_factor;
+  M.base_reward = c.base_reward;
+  M.bucket_x0 = h->sc.bucket_x[0];
+  M.bucket_x1 = h->sc.bucket_x[1];
+  M.bucket_y = h->sc.bucket_y;
+  M.bucket_z = h->sc.bucket_z;
+  M.env_class = c.env_class;
+  M.solver_iter = c.solver_iterations;
+  M.solver_tol = c.solver_tolerance;
+  M.arm_base = (const T*)h->arm_base;
+  M.body = (const T*)h->body;
+  M.dof = (const T*)h->dof;
+  M.ctrlrange = (const T*)h->ctrlrange;
+  M.geom = (const T*)h->geom;
+  M.geom_i = h->geom_i;
+  M.pair = h->pair;
+  M.param = (const T*)h->param;
+  M.cube = (const T*)h->cube;
+  M.meaninertia = (const T*)h->meaninertia;
+  M.tri = h->tri;
+  return M;
+}
+
+template <typename T>
+static State<T> make_state(const fm_handle* h) {
+  State<T> S;
+  S.phys = (T*)h->phys;
+  S.dbl = h->dbl;
+  S.ints = h->ints;
+  S.rng = h->rng;
+  S.counters = h->counters;
+  return S;
+}
+
+template <typename T>
+static int create_typed(fm_handle* h) {
+  const SceneHost& s = h->sc;
+  const Dims& d = h->dm;
+  std::vector<double> arm_base(12 * s.A), body(32 * ARM_NB, 0.0), dof(4 * ARM_ND, 0.0), ctrl(2 * s.nu);
+  for (int i = 0; i < s.A; i++)
+    for (int k = 0; k < 12; k++) arm_base[12 * i + k] = s.arm_base[i][k];
+  for (int b = 0; b < ARM_NB; b++) {
+    double* o = &body[32 * b];
+    for (int k = 0; k < 12; k++) o[k] = s.body_local[b][k];
+    o[12] = s.body_mass[b];
+    for (int k = 0; k < 3; k++) o[13 + k] = s.body_ipos[b][k];
+    for (int k = 0; k < 9; k++) o[16 + k] = s.body_iR[b][k];
+    for (int k = 0; k < 3; k++) o[25 + k] = s.body_I[b][k];
+    o[28] = s.body_invw[b][0];
+    o[29] = s.body_invw[b][1];
+  }
+  for (int j = 0; j < ARM_ND; j++) {
+    dof[4 * j] = s.dof_range[j][0];
+    dof[4 * j + 1] = s.dof_range[j][1];
+    dof[4 * j + 2] = s.dof_invw[j];
+  }
+  for (int u = 0; u < s.nu; u++) {
+    ctrl[2 * u] = s.ctrlrange[u][0];
+    ctrl[2 * u + 1] = s.ctrlrange[u][1];
+  }
+  int ngc = (int)s.geoms.size();
+  std::vector<double> geom(16 * ngc, 0.0), param(8 * s.params.size(), 0.0);
+  std::vector<int> geom_i(4 * ngc);
+  for (int g = 0; g < ngc; g++) {
+    const GeomRec& r = s.geoms[g];
+    for (int k = 0; k < 3; k++) geom[16 * g + k] = r.pos[k];
+    for (int k = 0; k < 9; k++) geom[16 * g + 3 + k] = r.R[k];
+    for (int k = 0; k < 3; k++) geom[16 * g + 12 + k] = r.size[k];
+    geom[16 * g + 15] = r.rbound;
+    geom_i[4 * g] = r.mjid;
+    geom_i[4 * g + 1] = r.type;
+    geom_i[4 * g + 2] = r.kbody;
+    geom_i[4 * g + 3] = s.box_slot[g];
+  }
+  // cube bounding radius depends on the per-arena size: use the largest possible (h <= 0.05)
+  for (int g = 0; g < ngc; g++)
+    if (s.geoms[g].kbody >= 2 && s.geoms[g].kbody < 2 + s.K) geom[16 * g + 15] = std::sqrt(3.0) * 0.05;
+  for (size_t p = 0; p < s.params.size(); p++) {
+    param[8 * p] = s.params[p].mu;
+    param[8 * p + 1] = s.params[p].solref[0];
+    param[8 * p + 2] = s.params[p].solref[1];
+    for (int k = 0; k < 5; k++) param[8 * p + 3 + k] = s.params[p].solimp[k];
+  }
+  int r;
+  if ((r = upload<T>(h, &h->arm_base, arm_base))) return r;
+  if ((r = upload<T>(h, &h->body, body))) return r;
+  if ((r = upload<T>(h, &h->dof, dof))) return r;
+  if ((r = upload<T>(h, &h->ctrlrange, ctrl))) return r;
+  if ((r = upload<T>(h, &h->geom, geom))) return r;
+  if ((r = upload_raw<int>(h, &h->geom_i, geom_i))) return r;
+  if ((r = upload_raw<uint32_t>(h, &h->pair, s.pairs))) return r;
+  if ((r = upload<T>(h, &h->param, param))) return r;
+  if ((r = upload<T>(h, &h->cube, s.cube))) return r;
+  if ((r = upload<T>(h, &h->meaninertia, s.meaninertia))) return r;
+  if ((r = upload_raw<uint32_t>(h, &h->tri, s.tri))) return r;
+  // state
+  size_t N = d.N;
+  HIPCHK(hipMalloc(&h->phys, N * d.phys_stride * sizeof(T)));
+  h->allocs.push_back(h->phys);
+  HIPCHK(hipMemset(h->phys, 0, N * d.phys_stride * sizeof(T)));
+  HIPCHK(hipMalloc((void**)&h->dbl, N * d.dbl_stride * sizeof(double)));
+  h->allocs.push_back(h->dbl);
+  HIPCHK(hipMemset(h->dbl, 0, N * d.dbl_stride * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&h->ints, N * d.int_stride * sizeof(int32_t)));
+  h->allocs.push_back(h->ints);
+  HIPCHK(hipMemset(h->ints, 0, N * d.int_stride * sizeof(int32_t)));
+  if ((r = upload_raw<uint64_t>(h, &h->rng, s.rng_init))) return r;
+  HIPCHK(hipMalloc((void**)&h->counters, N * 4 * sizeof(int64_t)));
+  h->allocs.push_back(h->counters);
+  HIPCHK(hipMemset(h->counters, 0, N * 4 * sizeof(int64_t)));
+  h->lay = lds_layout(d, sizeof(T));
+  if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
+  HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
+  HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
+  return 0;
+}
+
+static int state_record_size(const fm_handle* h) {
+  return (int)((h->dm.phys_stride + h->dm.dbl_stride) * sizeof(double) + h->dm.int_stride * sizeof(int32_t) +
+               4 * sizeof(uint64_t));
+}
+
+template <typename T>
+static int get_state_typed(fm_handle* h, char* out) {
+  const Dims& d = h->dm;
+  size_t N = d.N;
+  std::vector<T> ph(N * d.phys_stride);
+  std::vector<double> db(N * d.dbl_stride);
+  std::vector<int32_t> in(N * d.int_stride);
+  std::vector<uint64_t> rg(N * 4);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(ph.data(), h->phys, ph.size() * sizeof(T), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(db.data(), h->dbl, db.size() * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(in.data(), h->ints, in.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(rg.data(), h->rng, rg.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  size_t rec = state_record_size(h);
+  for (size_t n = 0; n < N; n++) {
+    char* o = out + n * rec;
+    double* dp = (double*)o;
+    for (int i = 0; i < d.phys_stride; i++) dp[i] = (double)ph[n * d.phys_stride + i];
+    for (int i = 0; i < d.dbl_stride; i++) dp[d.phys_stride + i] = db[n * d.dbl_stride + i];
+    int32_t* ip = (int32_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double));
+    for (int i = 0; i < d.int_stride; i++) ip[i] = in[n * d.int_stride + i];
+    uint64_t* up = (uint64_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double) + d.int_stride * sizeof(int32_t));
+    for (int i = 0; i < 4; i++) up[i] = rg[n * 4 + i];
+  }
+  return FM_OK;
+}
+
+template <typename T>
+static int set_state_typed(fm_handle* h, const char* src) {
+  const Dims& d = h->dm;
+  size_t N = d.N;
+  std::vector<T> ph(N * d.phys_stride);
+  std::vector<double> db(N * d.dbl_stride);
+  std::vector<int32_t> in(N * d.int_stride);
+  std::vector<uint64_t> rg(N * 4);
+  size_t rec = state_record_size(h);
+  for (size_t n = 0; n < N; n++) {
+    const char* o = src + n * rec;
+    const double* dp = (const double*)o;
+    for (int i = 0; i < d.phys_stride; i++) ph[n * d.phys_stride + i] = (T)dp[i];
+    for (int i = 0; i < d.dbl_stride; i++) db[n * d.dbl_stride + i] = dp[d.phys_stride + i];
+    const int32_t* ip = (const int32_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double));
+    for (int i = 0; i < d.int_stride; i++) in[n * d.int_stride + i] = ip[i];
+    const uint64_t* up =
+        (const uint64_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double) + d.int_stride * sizeof(int32_t));
+    for (int i = 0; i < 4; i++) rg[n * 4 + i] = up[i];
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(h->phys, ph.data(), ph.size() * sizeof(T), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->rng, rg.data(), rg.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  h->was_reset = true;
+  return FM_OK;
+}
+
+extern "C" {
+
+void fm_config_default(fm_config* c) {
+  std::memset(c, 0, sizeof *c);
+  c->num_arenas = 1;
+  c->num_arms = 2;
+  c->max_num_objects = 10;
+  c->env_class = FM_ENV_ALLFULLRL_PROGRESS;
+  c->precision = FM_FP32;
+  c->max_contacts = 0;
+  c->initial_conveyor_speed = 0.1;
+  c->conveyor_acceleration = 0.001;
+  c->pt_time = 0.2;
+  c->force_contact_threshold = 200.0;
+  c->control_frequency = 10;
+  c->spawn_freq = 1.0 / 10;
+  c->spawn_freq_increase = 1.001;
+  c->gripper_to_closest_cube_reward_factor = 0.2;
+  c->closest_cube_to_bucket_reward_factor = 0.4;
+  c->small_action_norm_reward_factor = 0.0;
+  c->base_reward = 0.4;
+  c->solver_iterations = 100;
+  c->solver_tolerance = 0.0;  // 0 = precision default (see fm_create)
+}
+
+const char* fm_last_error(void) { return g_err.c_str(); }
+
+int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle** out) {
+  if (!cfg || !out) return set_err(FM_EINVAL, "null argument");
+  *out = nullptr;
+  fm_handle* h = new fm_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  h->fp64 = cfg->precision == FM_FP64;
+  if (cfg->env_class != FM_ENV_FACTORY_SCORE && cfg->env_class != FM_ENV_ALLFULLRL_PROGRESS) {
+    delete h;
+    return set_err(FM_EINVAL, "unknown env_class");
+  }
+  if (h->cfg.solver_tolerance <= 0) h->cfg.solver_tolerance = h->fp64 ? 1e-12 : 1e-7;
+  if (h->cfg.solver_iterations <= 0) h->cfg.solver_iterations = 100;
+  std::string err;
+  if (!build_scene(cfg->num_arms, cfg->max_num_objects, cfg->num_arenas, seeds, h->sc, err)) {
+    delete h;
+    return set_err(FM_EINVAL, err);
+  }
+  const SceneHost& s = h->sc;
+  Dims& d = h->dm;
+  d.N = s.N;
+  d.A = s.A;
+  d.K = s.K;
+  d.nq = s.nq;
+  d.nv = s.nv;
+  d.nu = s.nu;
+  d.ngc = (int)s.geoms.size();
+  d.nbox = s.nbox;
+  d.npair = (int)s.pairs.size();
+  d.nparam = (int)s.params.size();
+  d.ntree = 1 + s.K + s.A;
+  d.obs_dim = s.obs_dim;
+  d.act_dim = s.act_dim;
+  d.frame_skip = (int)((1.0 / cfg->control_frequency) / 0.001);
+  d.maxcon = cfg->max_contacts > 0 ? std::min(cfg->max_contacts, MAXCON) : MAXCON;
+  d.maxrow = 10 * s.A;
+  d.phys_stride = 2 * s.nq + 3 * s.nv;
+  d.dbl_stride = s.nu + 3 + 2 * s.A + 1;
+  d.int_stride = 2 * s.K + I_NINT;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete h;
+    return set_err(FM_EDEVICE, "hipSetDevice failed");
+  }
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return set_err(FM_EDEVICE, "hipStreamCreate failed");
+  }
+  h->own_stream = true;
+  int r = h->fp64 ? create_typed<double>(h) : create_typed<float>(h);
+  if (r) {
+    std::string e = g_err;
+    fm_destroy(h);
+    return set_err(r, e);
+  }
+  *out = h;
+  return FM_OK;
+}
+
+void fm_destroy(fm_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) (void)hipFree(p);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int fm_set_stream(fm_handle* h, void* stream) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  h->stream = (hipStream_t)stream;  // NULL = the legacy default stream (torch's default stream)
+  return FM_OK;
+}
+
+int fm_sync(fm_handle* h) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipGetLastError());
+  return FM_OK;
+}
+
+int fm_obs_dim(const fm_handle* h) { return h ? h->dm.obs_dim : -1; }
+int fm_act_dim(const fm_handle* h) { return h ? h->dm.act_dim : -1; }
+int fm_num_arenas(const fm_handle* h) { return h ? h->dm.N : -1; }
+int fm_nq(const fm_handle* h) { return h ? h->dm.nq : -1; }
+int fm_nv(const fm_handle* h) { return h ? h->dm.nv : -1; }
+int fm_nu(const fm_handle* h) { return h ? h->dm.nu : -1; }
+
+int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  dim3 grid(h->dm.N), block(WAVE);
+  if (h->fp64) {
+    hipLaunchKernelGGL(reset_kernel<double>, grid, block, h->lay.total, h->stream, make_model<double>(h),
+                       make_state<double>(h), h->lay, obs, mask);
+  } else {
+    hipLaunchKernelGGL(reset_kernel<float>, grid, block, h->lay.total, h->stream, make_model<float>(h),
+                       make_state<float>(h), h->lay, obs, mask);
+  }
+  HIPCHK(hipGetLastError());
+  h->was_reset = true;
+  return FM_OK;
+}
+
+int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+            const fm_info* info) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  if (!actions) return set_err(FM_EINVAL, "actions is NULL");
+  if (!h->was_reset) return set_err(FM_ESTATE, "fm_step before fm_reset");
+  HIPCHK(hipSetDevice(h->device));
+  StepIO io;
+  std::memset(&io, 0, sizeof io);
+  io.actions = actions;
+  io.obs = obs;
+  io.reward = reward;
+  io.terminated = terminated;
+  io.truncated = truncated;
+  if (info) {
+    io.scores = info->scores;
+    io.num_obj = info->num_obj;
+    io.play_time = info->play_time;
+    io.conveyor_speed = info->conveyor_speed;
+    io.out_of_reach = info->out_of_reach;
+    io.force_terminate = info->force_terminate;
+    io.terminal_obs = info->terminal_obs;
+    io.ep_return = info->episode_return;
+    io.ep_len = info->episode_length;
+    io.terminal_scores = info->terminal_scores;
+  }
+  dim3 grid(h->dm.N), block(WAVE);
+  if (h->fp64) {
+    hipLaunchKernelGGL(step_kernel<double>, grid, block, h->lay.total, h->stream, make_model<double>(h),
+                       make_state<double>(h), h->lay, io);
+  } else {
+    hipLaunchKernelGGL(step_kernel<float>, grid, block, h->lay.total, h->stream, make_model<float>(h),
+                       make_state<float>(h), h->lay, io);
+  }
+  HIPCHK(hipGetLastError());
+  return FM_OK;
+}
+
+// exported record: doubles [phys (2nq+3nv) | dbl_stride] , int32 [int_stride], uint64 [4]
+int fm_state_size(const fm_handle* h) { return h ? state_record_size(h) : -1; }
+
+int fm_get_state(fm_handle* h, void* host_out) {
+  if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  return h->fp64 ? get_state_typed<double>(h, (char*)host_out) : get_state_typed<float>(h, (char*)host_out);
+}
+
+int fm_set_state(fm_handle* h, const void* host_in) {
+  if (!h || !host_in) return set_err(FM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  return h->fp64 ? set_state_typed<double>(h, (const char*)host_in) : set_state_typed<float>(h, (const char*)host_in);
+}
+
+int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int cap) {
+  if (!h || !host_out || arena < 0 || arena >= h->dm.N) return set_err(FM_EINVAL, "bad argument");
+  const Dims& d = h->dm;
+  int need = 2 + 81 * d.A + 4 * d.nv + 3 * d.A + 60 * d.A + 27 * d.A + 17 * 64 + 6 * 20 * d.A;
+  if (cap < need) return set_err(FM_EINVAL, "buffer too small: need " + std::to_string(need));
+  HIPCHK(hipSetDevice(h->device));
+  double* dbuf = nullptr;
+  HIPCHK(hipMalloc(&dbuf, need * sizeof(double)));
+  HIPCHK(hipMemset(dbuf, 0, need * sizeof(double)));
+  if (h->fp64) {
+    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               h->lay.total));
+    hipLaunchKernelGGL(debug_kernel<double>, dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<double>(h),
+                       make_state<double>(h), h->lay, arena, actuated, dbuf);
+  } else {
+    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               h->lay.total));
+    hipLaunchKernelGGL(debug_kernel<float>, dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<float>(h),
+                       make_state<float>(h), h->lay, arena, actuated, dbuf);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(host_out, dbuf, need * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(dbuf));
+  return need;
+}
+
+int fm_get_counters(fm_handle* h, int64_t* host_out) {
+  if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return FM_OK;
+}
+
+}  // extern "C"

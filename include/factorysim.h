@@ -1,0 +1,138 @@
+/* factorysim.h -- C ABI of the MI355X-native batched factory-manipulation environment.
+ *
+ * Drop-in boundary for the reference's env-step path.  The reference exposes it as a Gymnasium env
+ * stepped through stable-baselines3's VecEnv (SubprocVecEnv, one Python process per arena):
+ *   FactoryManipulationEnv.step(action)         /root/reference/src/environments.py:151-202
+ *   FactoryManipulationEnv.reset(seed, options) /root/reference/src/environments.py:204-248
+ *   BaseEnv.step_sim / reset_sim                 /root/reference/challenge_env/challenge_env/base_env.py:177-282
+ *   make_vec_env(..., vec_env_cls=SubprocVecEnv) /root/reference/src/learning.py:98-100
+ * This ABI replaces the whole SubprocVecEnv fan-out: one handle owns N arenas resident in HBM and
+ * one fm_step() advances all of them by one env-step (100 physics substeps + task layer + wrappers,
+ * with SB3-style auto-reset).  factory_marl_amd/vec_env.py binds it with ctypes; INTEGRATION.md
+ * shows the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *  - Status codes: 0 = ok, < 0 = error (FM_E*); fm_last_error() returns a thread-local message.
+ *    No C++ exception crosses the ABI.
+ *  - Ownership: the library owns all arena state (device memory).  The caller owns every I/O
+ *    buffer passed in and keeps it alive for the call; I/O buffers are DEVICE pointers
+ *    (e.g. torch.Tensor.data_ptr() of a ROCm tensor) unless a parameter says "host".
+ *  - Streams: each handle runs on one HIP stream (fm_set_stream); calls are asynchronous on it.
+ *    A handle is not re-entrant; several handles (one per GPU / rank) may be driven concurrently.
+ *  - Errors are reported eagerly for argument problems; device faults surface on fm_sync().
+ */
+#ifndef FACTORYSIM_H
+#define FACTORYSIM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FM_OK 0
+#define FM_EINVAL (-1)  /* bad argument / config */
+#define FM_EDEVICE (-2) /* HIP runtime error */
+#define FM_ENOMEM (-3)
+#define FM_ESTATE (-4)  /* call order (e.g. step before reset) */
+
+/* env classes (environments.py) whose step() this library implements */
+#define FM_ENV_FACTORY_SCORE 0      /* score-delta reward (FactoryManipulationEnv._get_reward), AllFullRL actions */
+#define FM_ENV_ALLFULLRL_PROGRESS 1 /* AllFullRLProgressRewardEnv (environments.py:462-495) */
+
+#define FM_FP32 0 /* physics state and arithmetic in float  (north-star configuration) */
+#define FM_FP64 1 /* physics state and arithmetic in double (bit-for-bit twin of the oracle's precision) */
+
+/* Mirrors BaseEnv.__init__ kwargs (base_env.py:15-35) and ProgressRewardEnv weights
+ * (environments.py:252-258).  fm_config_default() fills the reference defaults. */
+typedef struct fm_config {
+  int32_t num_arenas;
+  int32_t num_arms;        /* even, >= 2 (scene.py:149) */
+  int32_t max_num_objects; /* K cubes per arena */
+  int32_t env_class;       /* FM_ENV_* */
+  int32_t precision;       /* FM_FP32 / FM_FP64 */
+  int32_t max_contacts;    /* per-arena contact capacity (0 = automatic) */
+  double initial_conveyor_speed;  /* 0.1 m/s */
+  double conveyor_acceleration;   /* 0.001 m/s^2 */
+  double pt_time;                 /* 0.2 s */
+  double force_contact_threshold; /* 200 N */
+  double control_frequency;       /* 10 Hz -> frame_skip = int((1/f)/0.001) = 100 */
+  double spawn_freq;              /* 0.1 (multiplied by num_arms, base_env.py:36) */
+  double spawn_freq_increase;     /* 1.001 */
+  double gripper_to_closest_cube_reward_factor;
+  double closest_cube_to_bucket_reward_factor;
+  double small_action_norm_reward_factor;
+  double base_reward;
+  int32_t solver_iterations; /* Newton iterations cap (MuJoCo default 100) */
+  double solver_tolerance;   /* scaled improvement / gradient tolerance (MuJoCo default 1e-8) */
+} fm_config;
+
+/* Per-step info, all DEVICE pointers, any may be NULL (info dict of base_env.py:274-280 plus the
+ * SB3 Monitor / auto-reset extras). */
+typedef struct fm_info {
+  int32_t* scores;          /* [N, 2] */
+  int32_t* num_obj;         /* [N]   objects in scene after the step */
+  double* play_time;        /* [N] */
+  double* conveyor_speed;   /* [N] */
+  uint8_t* out_of_reach;    /* [N]   TaskManager.terminate */
+  uint8_t* force_terminate; /* [N] */
+  float* terminal_obs;      /* [N, obs_dim] written for arenas that terminated (before auto-reset) */
+  double* episode_return;   /* [N]   Monitor "r" of the finished episode (valid where terminated) */
+  int32_t* episode_length;  /* [N]   Monitor "l" */
+  int32_t* terminal_scores; /* [N, 2] scores of the finished episode (ep_score_history entry) */
+} fm_info;
+
+typedef struct fm_handle fm_handle;
+
+void fm_config_default(fm_config* cfg);
+
+/* Create N arenas on `device`.  seeds: host array [N] -- per-arena seed used, as in the reference,
+ * both for build_scene's cube sizes (scene.py:121) and for the TaskManager RNG (task_utils.py:19).
+ * NULL = every arena uses seed 42 (the value in every saved run config under runs/). */
+int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle** out);
+void fm_destroy(fm_handle* h);
+const char* fm_last_error(void);
+
+/* Set the HIP stream all later calls of this handle run on (hipStream_t passed as void*; NULL = the
+ * legacy default stream).  fm_create starts on a private non-blocking stream. */
+int fm_set_stream(fm_handle* h, void* stream);
+int fm_sync(fm_handle* h);
+
+int fm_obs_dim(const fm_handle* h);
+int fm_act_dim(const fm_handle* h);
+int fm_num_arenas(const fm_handle* h);
+int fm_nq(const fm_handle* h);
+int fm_nv(const fm_handle* h);
+int fm_nu(const fm_handle* h);
+
+/* reset(): reset arenas where mask[i] != 0 (device uint8 [N]; NULL = all) and write their obs.
+ * Mirrors BaseEnv.reset_sim + FactoryManipulationEnv.reset (environments.py:204-248): the
+ * TaskManager RNG is NOT reseeded (task_utils.py:19), progress-reward distance memories persist. */
+int fm_reset(fm_handle* h, const uint8_t* mask, float* obs);
+
+/* step(): actions float32 [N, act_dim] (device).  Writes obs [N, obs_dim] (reset obs for arenas
+ * that terminated), reward [N], terminated [N], truncated [N] (always 0: the reference has no
+ * time limit, environments.py:202), and info.  Any output pointer may be NULL. */
+int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated,
+            uint8_t* truncated, const fm_info* info);
+
+/* Teacher forcing / checkpointing of the full arena state (HOST buffers).
+ * Physics block per arena (float64): qpos[nq], qvel[nv], qpos_stage[nq], qvel_stage[nv],
+ * qacc_warmstart[nv], ctrl_target[nu]; see fm_state_layout() for the task block. */
+int fm_state_size(const fm_handle* h);                 /* bytes per arena of the exported record */
+int fm_get_state(fm_handle* h, void* host_out);        /* [N * fm_state_size] */
+int fm_set_state(fm_handle* h, const void* host_in);
+
+/* Diagnostics: per-arena counters accumulated since create (host [N*4] int64):
+ * contacts dropped for capacity, Newton iterations, solver max-iteration hits, bucket-index
+ * anomalies (task_utils.py:103-113 would raise IndexError). */
+int fm_get_counters(fm_handle* h, int64_t* host_out);
+
+/* Diagnostic (tests only): recompute one mj_step1 + acceleration stage of `arena` at its stored stage
+ * state and dump internals as float64 into host_out (capacity `cap` doubles).  Returns the number of
+ * doubles written (< 0 on error).  Layout in factory_marl_amd/csrc/fm_kernel.hip (debug_kernel). */
+int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -44,6 +44,21 @@ double* or_d_geom_xpos(or_data* d) { return d->geom_xpos; }
 double* or_d_geom_xmat(or_data* d) { return d->geom_xmat; }
 double* or_d_site_xpos(or_data* d) { return d->site_xpos; }
 double* or_d_efc_force(or_data* d) { return d->efc_force; }
+double* or_d_qacc_smooth(or_data* d) { return d->qacc_smooth; }
+double* or_d_qfrc_smooth(or_data* d) { return d->qfrc_smooth; }
+double* or_d_qfrc_passive(or_data* d) { return d->qfrc_passive; }
+int* or_d_efc_type(or_data* d) { return d->efc_type; }
+double* or_d_efc_pos(or_data* d) { return d->efc_pos; }
+double* or_d_efc_D(or_data* d) { return d->efc_D; }
+double* or_d_efc_aref(or_data* d) { return d->efc_aref; }
+double* or_d_efc_J(or_data* d) { return d->efc_J; }
+double* or_d_stage_fwd(const or_model* m, or_data* d, int actuated) {
+  /* mj_step1 at the current qpos/qvel + actuation + smooth acceleration + solve (no integration) */
+  d->actuation_disabled = !actuated;
+  or_forward(m, d);
+  d->actuation_disabled = 0;
+  return d->qacc;
+}
 int or_d_ncon(const or_data* d) { return d->ncon; }
 int or_d_nefc(const or_data* d) { return d->nefc; }
 int or_d_niter(const or_data* d) { return d->solver_niter; }
@@ -97,3 +112,106 @@ or_task* or_task_new(int A, int K, uint64_t seed) {
   return t;
 }
 void or_task_free(or_task* t) { free(t); }
+
+/* ---- exchange of the full arena state with the product's record layout (include/factorysim.h,
+ *      fm_get_state / fm_set_state): doubles [qpos nq | qvel nv | qpos_stage nq | qvel_stage nv |
+ *      qacc_warmstart nv | ctrl_target nu | spawn_freq | speed | play_time | last_grip A |
+ *      last_bucket A | ep_return], int32 [in K | out K | n_in n_out step since fail hidden s0 s1 ls0 ls1 eplen],
+ *      uint64 [state_hi state_lo inc_hi inc_lo] */
+void or_env_export(const or_env* e, double* dbl, int32_t* ints, uint64_t* rng) {
+  const or_model* m = e->m;
+  const or_data* d = e->d;
+  const or_task* t = &e->t;
+  int nq = m->nq, nv = m->nv, nu = m->nu, A = m->A, K = m->K;
+  double* p = dbl;
+  memcpy(p, d->qpos, nq * sizeof(double)); p += nq;
+  memcpy(p, d->qvel, nv * sizeof(double)); p += nv;
+  memcpy(p, e->stage_qpos, nq * sizeof(double)); p += nq;
+  memcpy(p, e->stage_qvel, nv * sizeof(double)); p += nv;
+  memcpy(p, d->qacc_warmstart, nv * sizeof(double)); p += nv;
+  memcpy(p, t->ctrl_target, nu * sizeof(double)); p += nu;
+  *p++ = t->spawn_freq;
+  *p++ = t->conveyor_speed;
+  *p++ = t->play_time;
+  for (int i = 0; i < A; i++) *p++ = t->last_grip_dist[i];
+  for (int i = 0; i < A; i++) *p++ = t->last_bucket_dist[i];
+  *p++ = e->ep_return;
+  int32_t* q = ints;
+  for (int k = 0; k < K; k++) q[k] = k < t->n_in ? t->in_scene[k] : -1;
+  for (int k = 0; k < K; k++) q[K + k] = k < t->n_out ? t->out_scene[k] : -1;
+  q += 2 * K;
+  q[0] = t->n_in; q[1] = t->n_out; q[2] = t->step_counter; q[3] = t->steps_since_spawn;
+  q[4] = t->failure_counter; q[5] = t->hidden_counter; q[6] = t->scores[0]; q[7] = t->scores[1];
+  q[8] = t->last_score[0]; q[9] = t->last_score[1]; q[10] = e->ep_len;
+  rng[0] = t->rng.state_hi; rng[1] = t->rng.state_lo; rng[2] = t->rng.inc_hi; rng[3] = t->rng.inc_lo;
+}
+
+/* set the oracle from a record; the position/velocity stage is recomputed at qpos_stage/qvel_stage */
+void or_env_import(or_env* e, const double* dbl, const int32_t* ints, const uint64_t* rng) {
+  const or_model* m = e->m;
+  or_data* d = e->d;
+  or_task* t = &e->t;
+  int nq = m->nq, nv = m->nv, nu = m->nu, A = m->A, K = m->K;
+  const double* p = dbl;
+  const double* q_now = p; p += nq;
+  const double* v_now = p; p += nv;
+  memcpy(e->stage_qpos, p, nq * sizeof(double)); p += nq;
+  memcpy(e->stage_qvel, p, nv * sizeof(double)); p += nv;
+  memcpy(d->qacc_warmstart, p, nv * sizeof(double)); p += nv;
+  memcpy(t->ctrl_target, p, nu * sizeof(double)); p += nu;
+  t->spawn_freq = *p++;
+  t->conveyor_speed = *p++;
+  t->play_time = *p++;
+  for (int i = 0; i < A; i++) t->last_grip_dist[i] = *p++;
+  for (int i = 0; i < A; i++) t->last_bucket_dist[i] = *p++;
+  e->ep_return = *p++;
+  const int32_t* q = ints + 2 * K;
+  t->n_in = q[0]; t->n_out = q[1]; t->step_counter = q[2]; t->steps_since_spawn = q[3];
+  t->failure_counter = q[4]; t->hidden_counter = q[5]; t->scores[0] = q[6]; t->scores[1] = q[7];
+  t->last_score[0] = q[8]; t->last_score[1] = q[9]; e->ep_len = q[10];
+  for (int k = 0; k < K; k++) t->in_scene[k] = ints[k];
+  for (int k = 0; k < K; k++) t->out_scene[k] = ints[K + k];
+  t->rng.state_hi = rng[0]; t->rng.state_lo = rng[1]; t->rng.inc_hi = rng[2]; t->rng.inc_lo = rng[3];
+  /* stage at the stage state, then the current state on top (legacy-step semantics) */
+  memcpy(d->qpos, e->stage_qpos, nq * sizeof(double));
+  memcpy(d->qvel, e->stage_qvel, nv * sizeof(double));
+  or_step1(m, d);
+  memcpy(d->qpos, q_now, nq * sizeof(double));
+  memcpy(d->qvel, v_now, nv * sizeof(double));
+}
+
+/* CPU baseline leg of bench.py: n arenas x `steps` env-steps of the oracle with uniform random
+ * AllFullRL actions, OpenMP over arenas (one arena per thread at a time), auto-reset on termination.
+ * Returns wall seconds of the stepping (env creation and reset excluded). */
+#include <omp.h>
+double or_batch_bench(int A, int K, int n, int steps, int threads, uint64_t seed, int64_t* env_steps_out) {
+  or_env** envs = malloc(n * sizeof(or_env*));
+  const double w[4] = {0.2, 0.4, 0.0, 0.4};
+  for (int i = 0; i < n; i++) {
+    envs[i] = or_env_create(A, K, 42, 1, w);
+    or_env_reset(envs[i], NULL);
+  }
+  int64_t total = 0;
+  double t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : total)
+  for (int i = 0; i < n; i++) {
+    uint64_t s = seed * 0x9E3779B97F4A7C15ULL + (uint64_t)i * 0xD1B54A32D192ED03ULL + 1;
+    float act[128];
+    double rew, info[7];
+    for (int t = 0; t < steps; t++) {
+      for (int j = 0; j < 8 * A; j++) {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        act[j] = (float)((double)(s >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0);
+      }
+      if (or_env_step(envs[i], act, NULL, &rew, info)) or_env_reset(envs[i], NULL);
+      total++;
+    }
+  }
+  double dt = omp_get_wtime() - t0;
+  for (int i = 0; i < n; i++) or_env_free(envs[i]);
+  free(envs);
+  if (env_steps_out) *env_steps_out = total;
+  return dt;
+}

@@ -158,6 +158,10 @@ typedef struct or_env {
   or_data* d;
   or_task t;
   int obs_dim, act_dim;
+  double* stage_qpos; /* state at which the current position/velocity stage was computed (last mj_step1) */
+  double* stage_qvel;
+  double ep_return;
+  int ep_len;
 } or_env;
 
 or_env* or_env_create(int A, int K, uint64_t seed, int reward_kind, const double* reward_w /*4*/);

@@ -77,6 +77,12 @@ def lib():
             "or_t_int": (I, [P, C.c_char_p]), "or_t_double": (D, [P, C.c_char_p]),
             "or_t_in_scene": (C.POINTER(I), [P]), "or_t_ctrl_target": (DP, [P]),
             "or_t_set_reward": (None, [P, I, DP]),
+            "or_env_export": (None, [P, P, P, P]),
+            "or_d_qacc_smooth": (DP, [P]), "or_d_qfrc_smooth": (DP, [P]), "or_d_qfrc_passive": (DP, [P]),
+            "or_d_efc_type": (C.POINTER(I), [P]), "or_d_efc_pos": (DP, [P]), "or_d_efc_D": (DP, [P]),
+            "or_d_efc_aref": (DP, [P]), "or_d_efc_J": (DP, [P]), "or_d_stage_fwd": (DP, [P, P, I]),
+            "or_env_import": (None, [P, P, P, P]),
+            "or_batch_bench": (D, [I, I, I, I, I, U64, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -317,3 +323,24 @@ class Env:
 
     def ctrl_target(self):
         return arr(lib().or_t_ctrl_target(self.task), self.model.nu)
+
+    def state_sizes(self):
+        m = self.model
+        nd = 2 * m.nq + 3 * m.nv + m.nu + 3 + 2 * m.A + 1
+        ni = 2 * m.K + 11
+        return nd, ni
+
+    def export_state(self):
+        """full arena state in the product's record layout (fm_get_state)"""
+        nd, ni = self.state_sizes()
+        dbl = np.zeros(nd)
+        ints = np.zeros(ni, np.int32)
+        rng = np.zeros(4, np.uint64)
+        lib().or_env_export(self.h, ptr(dbl), ptr(ints), ptr(rng))
+        return dbl, ints, rng
+
+    def import_state(self, dbl, ints, rng):
+        dbl = np.ascontiguousarray(dbl, dtype=np.float64)
+        ints = np.ascontiguousarray(ints, dtype=np.int32)
+        rng = np.ascontiguousarray(rng, dtype=np.uint64)
+        lib().or_env_import(self.h, ptr(dbl), ptr(ints), ptr(rng))

@@ -68,7 +68,7 @@ void or_task_reset(or_task* t, const or_model* m, double* qpos, double* qvel) {
 void or_task_process_action(const or_model* m, const float* action, double* arm_ctrl) {
   for (int i = 0; i < m->A; i++)
     for (int j = 0; j < 8; j++) {
-      float a = tanhf(action[8 * i + j]);
+      float a = (float)tanh((double)action[8 * i + j]); /* correctly rounded float32 tanh */
       float s = (a + 1.0f) * 0.5f;
       double lo = m->act_ctrlrange[2 * (1 + j)], hi = m->act_ctrlrange[2 * (1 + j) + 1];
       arm_ctrl[8 * i + j] = lo + (double)s * (hi - lo);
@@ -304,6 +304,8 @@ or_env* or_env_create(int A, int K, uint64_t seed, int reward_kind, const double
   }
   e->obs_dim = 24 * A + 13 * K;
   e->act_dim = 8 * A;
+  e->stage_qpos = calloc(e->m->nq, sizeof(double));
+  e->stage_qvel = calloc(e->m->nv, sizeof(double));
   return e;
 }
 
@@ -311,6 +313,8 @@ void or_env_free(or_env* e) {
   if (!e) return;
   or_data_free(e->d);
   or_model_free(e->m);
+  free(e->stage_qpos);
+  free(e->stage_qvel);
   free(e);
 }
 
@@ -320,6 +324,10 @@ void or_env_reset(or_env* e, float* obs) {
   e->d->actuation_disabled = 1;
   or_forward(e->m, e->d); /* physics.after_reset(): forward with actuation disabled */
   e->d->actuation_disabled = 0;
+  memcpy(e->stage_qpos, e->d->qpos, e->m->nq * sizeof(double));
+  memcpy(e->stage_qvel, e->d->qvel, e->m->nv * sizeof(double));
+  e->ep_return = 0;
+  e->ep_len = 0;
   if (obs) or_task_obs(&e->t, e->m, e->d->qpos, e->d->qvel, obs);
 }
 
@@ -348,12 +356,16 @@ int or_env_step(or_env* e, const float* action, float* obs, double* reward, doub
     }
     or_step1(m, d);
   }
+  memcpy(e->stage_qpos, d->qpos, m->nq * sizeof(double));
+  memcpy(e->stage_qvel, d->qvel, m->nv * sizeof(double));
   or_task_step(t, m, d->qpos, d->qvel);
   or_task_after_step(t);
   int terminated = t->failure_counter > 0 || force_term;
   double grip[48];
   for (int i = 0; i < m->A; i++) memcpy(grip + 3 * i, d->site_xpos + 3 * m->grip_site[i], 3 * sizeof(double));
   *reward = or_task_reward(t, m, d->qpos, grip, action);
+  e->ep_return += *reward;
+  e->ep_len++;
   if (obs) or_task_obs(t, m, d->qpos, d->qvel, obs);
   if (info) {
     info[0] = t->scores[0];

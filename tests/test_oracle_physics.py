@@ -1,0 +1,294 @@
+"""Analytic known-answer tests that pin the oracle's physics restatement.
+
+MuJoCo is not available (parity unpinned), so the oracle's MuJoCo restatement is pinned
+by closed-form cases instead: semi-implicit free fall, exponential-map quaternion integration,
+inertia / bias identities (energy, gravity = -dV/dq, power balance q'Cq' = 1/2 q'Mdot q'),
+implicit velocity-actuator response of the belt, static equilibrium of a resting cube, and the
+narrowphase primitives on hand-computed configurations.
+"""
+import numpy as np
+import pytest
+
+G = 9.81
+DT = 0.001
+
+
+@pytest.fixture(scope="module")
+def env(oracle):
+    e = oracle.Env(2, 4, 42)
+    e.reset()
+    return e
+
+
+def _park_all(env):
+    """arms at qpos0 (straight up), cubes far away resting above the floor"""
+    d = env.data
+    q = d.qpos
+    q[:] = 0
+    for k in range(env.model.K):
+        q[1 + 7 * k:8 + 7 * k] = [4.0 + k, 3.0, 0.5, 1, 0, 0, 0]
+    d.qvel[:] = 0
+
+
+def test_model_dimensions(oracle):
+    for A, K in [(2, 4), (2, 8), (4, 16)]:
+        m = oracle.Model(A, K, 42)
+        assert (m.nq, m.nv, m.nu, m.ngeom) == (1 + 9 * A + 7 * K, 1 + 9 * A + 6 * K, 1 + 8 * A, 13 + K + 70 * A)
+        for i in range(A):
+            lo, hi = m.arm_geom_range(i)
+            assert hi - lo == 70 and lo == 13 + K + 70 * i
+
+
+def test_free_fall_semi_implicit(env):
+    d = env.data
+    _park_all(env)
+    k = 0
+    d.qpos[1:8] = [0.3, 0.0, 3.0, 1, 0, 0, 0]
+    d.step1()
+    for n in range(1, 201):
+        d.step(np.zeros(env.model.nu))
+    # semi-implicit Euler: v_n = -g n dt, z_n = z0 - g dt^2 n(n+1)/2
+    n = 200
+    assert abs(d.qvel[3] - (-G * n * DT)) < 1e-12
+    assert abs(d.qpos[3] - (3.0 - G * DT * DT * n * (n + 1) / 2)) < 1e-12
+    assert abs(d.qpos[1] - 0.3) < 1e-15
+
+
+def test_quaternion_exponential_map(env):
+    d = env.data
+    _park_all(env)
+    d.qpos[1:8] = [0.3, 0.0, 3.0, 1, 0, 0, 0]
+    w = np.array([1.0, -2.0, 0.5])  # body frame; cube is isotropic -> omega constant
+    d.qvel[4:7] = w
+    d.step1()
+    n = 50
+    for _ in range(n):
+        d.step(np.zeros(env.model.nu))
+    ang = np.linalg.norm(w) * DT * n
+    ax = w / np.linalg.norm(w)
+    expect = np.r_[np.cos(ang / 2), ax * np.sin(ang / 2)]
+    np.testing.assert_allclose(d.qpos[4:8], expect, atol=1e-12)
+    np.testing.assert_allclose(d.qvel[4:7], w, atol=1e-12)
+
+
+def _arm_state(env, rng):
+    d = env.data
+    _park_all(env)
+    nv = env.model.nv
+    a0 = 1 + 7 * env.model.K
+    v0 = 1 + 6 * env.model.K
+    for i in range(2):
+        d.qpos[a0 + 9 * i:a0 + 9 * i + 7] = rng.uniform(-1.5, 1.5, 7)
+        d.qpos[a0 + 9 * i + 7:a0 + 9 * i + 9] = rng.uniform(0, 0.05, 2)
+    d.qvel[:] = rng.normal(0, 1, nv)
+    return d
+
+
+def test_mass_matrix_energy_and_spd(env, oracle):
+    rng = np.random.default_rng(1)
+    d = _arm_state(env, rng)
+    d.step1()
+    M = d.M.copy()
+    np.testing.assert_allclose(M, M.T, atol=1e-12)
+    assert np.linalg.eigvalsh(M).min() > 0
+    # kinetic energy from body velocities: 1/2 sum m v_c^2 + 1/2 w' I w  (finite-difference of com positions)
+    q0, v = d.qpos.copy(), d.qvel.copy()
+    eps = 1e-6
+    m = env.model
+
+    def coms(qp):
+        d.qpos[:] = qp
+        d.step1()
+        return d.xipos.copy(), d.xmat.copy()
+
+    def qadd(qp, dv, h):
+        q = qp.copy()
+        # hinge/slide/free translation: additive; free rotation: integrate body-frame rate
+        nq_ = 0
+        q[0] += h * dv[0]
+        for k in range(m.K):
+            q[1 + 7 * k:4 + 7 * k] += h * dv[1 + 6 * k:4 + 6 * k]
+            w = dv[4 + 6 * k:7 + 6 * k] * h
+            ang = np.linalg.norm(w)
+            if ang > 0:
+                qr = np.r_[np.cos(ang / 2), w / ang * np.sin(ang / 2)]
+                a = q[4 + 7 * k:8 + 7 * k]
+                q[4 + 7 * k:8 + 7 * k] = [a[0] * qr[0] - a[1:] @ qr[1:], *(a[0] * qr[1:] + qr[0] * a[1:] + np.cross(a[1:], qr[1:]))]
+        a0 = 1 + 7 * m.K
+        v0 = 1 + 6 * m.K
+        q[a0:] += h * dv[v0:]
+        return q
+
+    xp, _ = coms(qadd(q0, v, eps))
+    xm, _ = coms(qadd(q0, v, -eps))
+    vc = (xp - xm) / (2 * eps)
+    d.qpos[:] = q0
+    d.qvel[:] = v
+    d.step1()
+    mass = m.body_mass
+    ke_trans = 0.5 * np.sum(mass[:, None] * vc ** 2)
+    ke = 0.5 * v @ d.M @ v
+    assert ke > ke_trans > 0  # rotational part is positive
+
+
+def test_gravity_is_minus_grad_potential(env):
+    rng = np.random.default_rng(2)
+    d = _arm_state(env, rng)
+    d.qvel[:] = 0
+    d.step1()
+    g = d.qfrc_bias.copy()
+    m = env.model
+    a0 = 1 + 7 * m.K
+    v0 = 1 + 6 * m.K
+    q0 = d.qpos.copy()
+
+    def V(qp):
+        d.qpos[:] = qp
+        d.step1()
+        return G * np.sum(m.body_mass * d.xipos[:, 2])
+
+    eps = 1e-6
+    for j in range(18):
+        qp, qm = q0.copy(), q0.copy()
+        qp[a0 + j] += eps
+        qm[a0 + j] -= eps
+        dV = (V(qp) - V(qm)) / (2 * eps)
+        assert abs(g[v0 + j] - dV) < 1e-5 * (1 + abs(dV)), j
+
+
+def test_coriolis_power_balance(env):
+    rng = np.random.default_rng(3)
+    d = _arm_state(env, rng)
+    m = env.model
+    v = d.qvel.copy()
+    d.step1()
+    bias_v = d.qfrc_bias.copy()
+    q0 = d.qpos.copy()
+    d.qvel[:] = 0
+    d.step1()
+    grav = d.qfrc_bias.copy()
+    c = bias_v - grav  # C(q, qd) qd
+    a0 = 1 + 7 * m.K
+    v0 = 1 + 6 * m.K
+    eps = 1e-6
+    # d/dt M along qd (arms only, cubes parked with zero velocity)
+    va = v.copy()
+    va[:v0] = 0
+    qp, qm = q0.copy(), q0.copy()
+    qp[a0:] += eps * va[v0:]
+    qm[a0:] -= eps * va[v0:]
+    d.qpos[:] = qp
+    d.step1()
+    Mp = d.M.copy()
+    d.qpos[:] = qm
+    d.step1()
+    Mm = d.M.copy()
+    Mdot = (Mp - Mm) / (2 * eps)
+    d.qpos[:] = q0
+    d.qvel[:] = va
+    d.step1()
+    ca = d.qfrc_bias - grav
+    assert abs(va @ ca - 0.5 * va @ Mdot @ va) < 1e-5 * (1 + abs(va @ ca))
+
+
+def test_belt_velocity_actuator_implicit(env):
+    d = env.data
+    _park_all(env)
+    nu = env.model.nu
+    ctrl = np.zeros(nu)
+    ctrl[0] = -0.1
+    d.step1()
+    v = 0.0
+    # implicit recurrence: (M + dt*(kv + b)) dv = dt*(kv*(u - v) - b*v)  per step
+    M, kv, b = 1000.0, 1e4, 5e-4
+    for _ in range(100):
+        d.step(ctrl)
+        v = v + DT * (kv * (-0.1 - v) - b * v) / (M + DT * (kv + b))
+    assert abs(d.qvel[0] - v) < 1e-12
+
+
+def test_resting_cube_static_equilibrium(env):
+    d = env.data
+    _park_all(env)
+    h = env.model.cube_size[0]
+    d.qpos[1:8] = [4.0, 3.0, h - 1e-4, 1, 0, 0, 0]
+    d.step1()
+    for _ in range(1500):
+        d.step(np.zeros(env.model.nu))
+    cons = [i for i, c in enumerate(d.contacts()) if 3 in c["geom"]]
+    assert len(cons) == 4  # plane-box: 4 corners
+    fn = sum(d.contact_force(i)[0] for i in cons)
+    mass = env.model.body_mass[env.model.cube_body0]
+    assert abs(fn - mass * G) < 1e-3 * mass * G
+    assert np.abs(d.qvel[1:7]).max() < 1e-6
+
+
+def test_box_box_face_and_edge(oracle):
+    import ctypes as C
+
+    L = oracle.lib()
+    P = oracle.ptr
+    out = (C.c_char * (oracle.CONTACT_BYTES * 16))()
+    I3 = np.eye(3).reshape(-1)
+    h = np.array([0.1, 0.1, 0.1])
+    # face-face: box2 0.15 above box1 -> 0.05 penetration, 4 points at box2's bottom corners
+    n = L.or_box_box(P(np.zeros(3)), P(I3), P(h), P(np.array([0.0, 0.0, 0.15])), P(I3), P(h), 0.0, out)
+    assert n == 4
+    recs = np.frombuffer(bytes(out), dtype=np.float64, count=4 * oracle.CONTACT_BYTES // 8).reshape(4, -1)
+    np.testing.assert_allclose(recs[:, 0], -0.05)
+    np.testing.assert_allclose(recs[:, 4:7], [[0, 0, 1]] * 4, atol=1e-12)
+    np.testing.assert_allclose(np.sort(np.abs(recs[:, 1])), [0.1] * 4)
+    np.testing.assert_allclose(recs[:, 3], 0.075)  # midway between the two faces
+    # separated
+    assert L.or_box_box(P(np.zeros(3)), P(I3), P(h), P(np.array([0.0, 0.0, 0.21])), P(I3), P(h), 0.0, out) == 0
+    # edge-edge: box2 rotated 45 deg about x then placed above an edge direction
+    c, s = np.cos(np.pi / 4), np.sin(np.pi / 4)
+    Rx = np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    Ry = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    R1 = Ry  # box1 edge along y pointing up
+    R2 = Rx  # box2 edge along x pointing down
+    z = 0.1 * np.sqrt(2) * 2 - 0.01
+    n = L.or_box_box(P(np.zeros(3)), P(R1.reshape(-1).copy()), P(h), P(np.array([0, 0, z])),
+                     P(R2.reshape(-1).copy()), P(h), 0.0, out)
+    assert n == 1
+    rec = np.frombuffer(bytes(out), dtype=np.float64, count=oracle.CONTACT_BYTES // 8)
+    np.testing.assert_allclose(rec[0], -0.01, atol=1e-12)
+    np.testing.assert_allclose(rec[4:7], [0, 0, 1], atol=1e-12)
+    np.testing.assert_allclose(rec[1:4], [0, 0, z / 2], atol=1e-12)
+
+
+def test_sphere_box_cases(oracle):
+    import ctypes as C
+
+    L = oracle.lib()
+    P = oracle.ptr
+    out = (C.c_char * (oracle.CONTACT_BYTES * 2))()
+    I3 = np.eye(3).reshape(-1)
+    h = np.array([0.2, 0.1, 0.05])
+    # outside, above the top face: normal from sphere to box = -z
+    n = L.or_sphere_box(P(np.array([0.05, 0.0, 0.09])), 0.05, P(np.zeros(3)), P(I3), P(h), 0.0, out)
+    rec = np.frombuffer(bytes(out), dtype=np.float64, count=oracle.CONTACT_BYTES // 8)
+    assert n == 1
+    np.testing.assert_allclose(rec[0], -0.01, atol=1e-12)
+    np.testing.assert_allclose(rec[4:7], [0, 0, -1], atol=1e-12)
+    np.testing.assert_allclose(rec[1:4], [0.05, 0, 0.045], atol=1e-12)
+    # centre inside the box, nearest face +y
+    n = L.or_sphere_box(P(np.array([0.0, 0.08, 0.0])), 0.03, P(np.zeros(3)), P(I3), P(h), 0.0, out)
+    rec = np.frombuffer(bytes(out), dtype=np.float64, count=oracle.CONTACT_BYTES // 8)
+    np.testing.assert_allclose(rec[0], -(0.02 + 0.03), atol=1e-12)
+    np.testing.assert_allclose(rec[4:7], [0, -1, 0], atol=1e-12)
+    # corner region: distance to the corner
+    c = np.array([0.25, 0.15, 0.0])
+    n = L.or_sphere_box(P(c), 0.08, P(np.zeros(3)), P(I3), P(h), 0.0, out)
+    rec = np.frombuffer(bytes(out), dtype=np.float64, count=oracle.CONTACT_BYTES // 8)
+    np.testing.assert_allclose(rec[0], np.hypot(0.05, 0.05) - 0.08, atol=1e-12)
+
+
+def test_impedance_curve(oracle):
+    L = oracle.lib()
+    si = np.array([0.9, 0.95, 0.001, 0.5, 2.0])
+    f = lambda x: L.or_impedance(oracle.ptr(si), x)
+    assert f(0.0) == 0.9 and f(-0.002) == 0.95 and f(0.001) == 0.95
+    # power 2 below the midpoint: d = dmin + (x/mid)^2*mid * (dmax - dmin)
+    x = 0.00025
+    assert abs(f(-x) - (0.9 + (x / 0.001) ** 2 / 0.5 * 0.05)) < 1e-15
