@@ -57,7 +57,7 @@ class FmInfo(C.Structure):
 EXPORTED = [
     "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_reset", "fm_step", "fm_state_size",
-    "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump",
+    "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile",
 ]
 
 _LIB = None
@@ -103,6 +103,8 @@ def load():
     L.fm_get_counters.restype = I
     L.fm_debug_dump.argtypes = [P, I, I, P, I]
     L.fm_debug_dump.restype = I
+    L.fm_profile.argtypes = [P, I, P]
+    L.fm_profile.restype = I
     _LIB = L
     return L
 

@@ -15,6 +15,7 @@ constexpr int MAXPC = 8;      // contacts per geom pair (box-box)
 // Flat per-arena record layouts (strides in elements)
 struct Dims {
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
+  int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
   int phys_stride;  // T:      qpos nq | qvel nv | qpos_s nq | qvel_s nv | qacc_ws nv
   int dbl_stride;   // double: ctrl_target nu | spawn_freq | speed | play_time | last_grip A | last_bucket A | ep_return
@@ -43,12 +44,19 @@ struct Model {
   // geoms (compact, collidable)
   const T* geom;      // [ngc][16]  pos(3) R(9) size(3) rbound
   const int* geom_i;  // [ngc][4]   mjid, type, kbody, box slot
-  const uint32_t* pair;  // [npair]  c1 | c2 << 12 | param << 24
+  const uint32_t* pair;  // [npair]  c1 | c2 << 12 | param << 24 (reference list; the kernel uses cb*)
+  const int* ginfo;      // [ngc] packed: type code | arm << 2 | pclass << 3 | kbody << 8
+  const int* cbi;        // [ncb][4] kbody, flags, first index in cbg, geom count
+  const T* cbs;          // [ncb][8] static AABB centre(3), radius, half extents(3), pad
+  const uint16_t* cbg;   // geoms grouped by collision body
+  const uint32_t* cbp;   // [ncbp] allowed collision-body pairs b1 | b2 << 8
+  int ptab[25];          // param index by (pclass g1, pclass g2)
   const T* param;     // [nparam][8] mu, solref(2), solimp(5)
   // per arena
   const T* cube;      // [N][K][4] h, m, I, pad
   const T* meaninertia;  // [N]
   const uint32_t* tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
+  unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
 };
 
 template <typename T>
@@ -87,18 +95,22 @@ struct Lay {
   int bpos, bR, bcom, bIw, bF, bN, dax, danc, site;
   int cR;
   int Marm, Larm, LBarm;
-  int gx, gR;
+  int gx;     // T [ngc][4]  geom world centre, rbound
+  int ginfo, cbi, cbw, cbg;  // LDS copies of the geom / collision-body tables, body bounds T [ncb][8]
+  int sp, spoff, gsurv;      // broadphase work lists
+  int stage, skey, spw;      // staged contacts T [maxcon][8], keys, pair words
+  int cube;                  // T [K][4] this arena's cube h, m, I
   int H;
   int c_i;    // int [maxcon][4]: g1 | g2 << 12, tree1, tree2, flags
   int c_r;    // T [maxcon][CR]
   int r_i;    // int [maxrow][4]
   int r_r;    // T [maxrow][8]
-  int surv;   // uint16 [MAXSURV]
   int tmask;  // uint64 [ntree]
   int misc;   // int [16]
   int sort;   // int [K]
   int uctl;   // double [nu]  clipped control of this env-step
   int scal;   // double [4]   per-step scalars broadcast from lane 0
+  int prof;   // uint64 [16]  phase clocks of this arena (profiling only)
   int total;
 };
 
@@ -107,7 +119,12 @@ enum { CR_DIST = 0, CR_MU, CR_D, CR_KD, CR_BD, CR_POS, CR_FR = CR_POS + 3, CR_J 
        CR_JA = CR_VEL + 3, CR_JD = CR_JA + 3, CR_F = CR_JD + 3, CR_N = CR_F + 4 };
 // generic row record (equality / joint limit)
 enum { RR_C0 = 0, RR_C1, RR_POS, RR_D, RR_AREF, RR_JAR, RR_JD, RR_F, RR_N };
-enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG };
+// phase slots of the optional wall-clock profile (fm_profile)
+enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_NHESS, PH_NCHOL, PH_NSOLVE, PH_NLS,
+       PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_LAST };
+enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE };
+// packed geom info
+enum { GC_PLANE = 0, GC_SPHERE = 1, GC_BOX = 2, GI_ARM = 2, GI_PC = 3 };
 
 // ------------------------------------------------------------------------------------------------
 // math helpers

@@ -68,19 +68,43 @@ struct Ws {
   __device__ T* Larm() const { return (T*)(base + L->Larm); }
   __device__ T* LBarm() const { return (T*)(base + L->LBarm); }
   __device__ T* gx() const { return (T*)(base + L->gx); }
-  __device__ T* gR() const { return (T*)(base + L->gR); }
+  __device__ int* ginfo() const { return (int*)(base + L->ginfo); }
+  __device__ int* cbi() const { return (int*)(base + L->cbi); }
+  __device__ T* cbw() const { return (T*)(base + L->cbw); }
+  __device__ uint16_t* cbg() const { return (uint16_t*)(base + L->cbg); }
+  __device__ uint32_t* sp() const { return (uint32_t*)(base + L->sp); }
+  __device__ int* spoff() const { return (int*)(base + L->spoff); }
+  __device__ uint32_t* gsurv() const { return (uint32_t*)(base + L->gsurv); }
+  __device__ T* stage() const { return (T*)(base + L->stage); }
+  __device__ int* skey() const { return (int*)(base + L->skey); }
+  __device__ uint32_t* spw() const { return (uint32_t*)(base + L->spw); }
+  __device__ T* cube() const { return (T*)(base + L->cube); }
   __device__ T* H() const { return (T*)(base + L->H); }
   __device__ int* ci() const { return (int*)(base + L->c_i); }
   __device__ T* cr() const { return (T*)(base + L->c_r); }
   __device__ int* ri() const { return (int*)(base + L->r_i); }
   __device__ T* rr() const { return (T*)(base + L->r_r); }
-  __device__ uint16_t* surv() const { return (uint16_t*)(base + L->surv); }
   __device__ uint64_t* tmask() const { return (uint64_t*)(base + L->tmask); }
   __device__ int* misc() const { return (int*)(base + L->misc); }
   __device__ int* sortidx() const { return (int*)(base + L->sort); }
   __device__ double* uctl() const { return (double*)(base + L->uctl); }
   __device__ double* scal() const { return (double*)(base + L->scal); }
+  __device__ unsigned long long* prof() const { return (unsigned long long*)(base + L->prof); }
 };
+
+// optional phase profile: lane 0 charges the wall-clock time since the previous mark to phase k
+#define PMARK(k)                                                   \
+  do {                                                             \
+    if (M.prof) {                                                  \
+      SYNC();                                                      \
+      if (LANE == 0) {                                             \
+        unsigned long long _n = wall_clock64();                    \
+        unsigned long long* _p = w.prof();                         \
+        _p[k] += _n - _p[PH_LAST];                                 \
+        _p[PH_LAST] = _n;                                          \
+      }                                                            \
+    }                                                              \
+  } while (0)
 
 // ------------------------------------------------------------------------------------------------
 // tree / dof helpers
@@ -105,7 +129,7 @@ __device__ __forceinline__ int dof_tree(const Dims& d, int i) {
 // impedance / reference acceleration parameters (MuJoCo getimpedance, getKBIP with refsafe)
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__device__ T impedance(const T* si, T x) {
+__device__ __forceinline__ T impedance(const T* si, T x) {
   T dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
   const T lo = T(0.0001), hi = T(0.9999);
   dmin = dmin < lo ? lo : (dmin > hi ? hi : dmin);
@@ -125,7 +149,7 @@ __device__ T impedance(const T* si, T x) {
 }
 
 template <typename T>
-__device__ void kb_params(T dt, const T* solref, const T* solimp, T& K, T& B) {
+__device__ __forceinline__ void kb_params(T dt, const T* solref, const T* solimp, T& K, T& B) {
   T tc = solref[0], dr = solref[1];
   T dmax = solimp[1];
   dmax = dmax < T(0.0001) ? T(0.0001) : (dmax > T(0.9999) ? T(0.9999) : dmax);
@@ -144,76 +168,87 @@ __device__ void kb_params(T dt, const T* solref, const T* solimp, T& K, T& B) {
 // ------------------------------------------------------------------------------------------------
 // narrowphase (definitions identical to oracle/collide.c; normal from geom1 to geom2)
 // ------------------------------------------------------------------------------------------------
+// Contacts are emitted straight into the LDS staging area (slot = LDS atomic), tagged with a key
+// (canonical geom pair << 3 | index within the pair); collide() sorts them by key afterwards, so the
+// contact order equals the oracle's pair order whatever order the lanes emitted in.
 template <typename T>
-struct Con {
-  T dist, pos[3], n[3];
+struct Emit {
+  T* st;         // staging [cap][8]: dist pos(3) n(3)
+  int* keys;     // [cap]
+  uint32_t* pw;  // [cap] type-ordered pair word (c1 | c2 << 12 | param << 24)
+  int* cnt;
+  int cap;
+  int key;
+  uint32_t pair;
+  int sub;
+  __device__ void operator()(T dist, T p0, T p1, T p2, T n0, T n1, T n2) {
+    if (sub >= MAXPC) return;
+    int s = atomicAdd(cnt, 1);
+    if (s < cap) {
+      T* r = st + 8 * s;
+      r[0] = dist;
+      r[1] = p0;
+      r[2] = p1;
+      r[3] = p2;
+      r[4] = n0;
+      r[5] = n1;
+      r[6] = n2;
+      keys[s] = key | sub;
+      pw[s] = pair;
+    }
+    sub++;
+  }
 };
 
-template <typename T>
-__device__ int np_plane_sphere(const T* c, T r, Con<T>* out) {
+template <typename T, typename E>
+__device__ __forceinline__ void np_plane_sphere(const T* c, T r, E& emit) {
   // floor plane: origin, normal +z (scene.xml:21)
   T dist = c[2] - r;
-  if (dist > T(0)) return 0;
-  out[0].dist = dist;
-  out[0].n[0] = 0;
-  out[0].n[1] = 0;
-  out[0].n[2] = 1;
-  out[0].pos[0] = c[0];
-  out[0].pos[1] = c[1];
-  out[0].pos[2] = c[2] - (r + dist / T(2));
-  return 1;
+  if (dist > T(0)) return;
+  emit(dist, c[0], c[1], c[2] - (r + dist / T(2)), T(0), T(0), T(1));
 }
 
-template <typename T>
-__device__ int np_plane_box(const T* p, const T* R, const T* h, Con<T>* out) {
+template <typename T, typename E>
+__device__ __forceinline__ void np_plane_box(const T* p, const T* R, const T* h, E& emit) {
   T dist = p[2];
   int cnt = 0;
+#pragma unroll
   for (int i = 0; i < 8; i++) {
     T cl[3] = {(i & 1) ? h[0] : -h[0], (i & 2) ? h[1] : -h[1], (i & 4) ? h[2] : -h[2]};
     T cw[3];
     matvec3(R, cl, cw);
     T ld = cw[2];
-    if (dist + ld > T(0) || ld > T(0)) continue;
+    if (dist + ld > T(0) || ld > T(0) || cnt >= 4) continue;
     T cd = dist + ld;
-    out[cnt].dist = cd;
-    out[cnt].n[0] = 0;
-    out[cnt].n[1] = 0;
-    out[cnt].n[2] = 1;
-    out[cnt].pos[0] = cw[0] + p[0];
-    out[cnt].pos[1] = cw[1] + p[1];
-    out[cnt].pos[2] = cw[2] + p[2] - cd / T(2);
-    if (++cnt >= 4) return 4;
+    emit(cd, cw[0] + p[0], cw[1] + p[1], cw[2] + p[2] - cd / T(2), T(0), T(0), T(1));
+    cnt++;
   }
-  return cnt;
 }
 
-template <typename T>
-__device__ int np_sphere_sphere(const T* c1, T r1, const T* c2, T r2, Con<T>* out) {
+template <typename T, typename E>
+__device__ __forceinline__ void np_sphere_sphere(const T* c1, T r1, const T* c2, T r2, E& emit) {
   T n[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
   T len = sqrt(dot3(n, n));
   T dist = len - r1 - r2;
-  if (dist > T(0)) return 0;
+  if (dist > T(0)) return;
   if (len < T(1e-15)) {
     n[0] = 1;
     n[1] = n[2] = 0;
   } else {
     for (int k = 0; k < 3; k++) n[k] /= len;
   }
-  out[0].dist = dist;
-  for (int k = 0; k < 3; k++) {
-    out[0].n[k] = n[k];
-    out[0].pos[k] = c1[k] + n[k] * (r1 + dist / T(2));
-  }
-  return 1;
+  T s = r1 + dist / T(2);
+  emit(dist, c1[0] + n[0] * s, c1[1] + n[1] * s, c1[2] + n[2] * s, n[0], n[1], n[2]);
 }
 
-template <typename T>
-__device__ int np_sphere_box(const T* c, T r, const T* p, const T* R, const T* h, Con<T>* out) {
+template <typename T, typename E>
+__device__ __forceinline__ void np_sphere_box(const T* c, T r, const T* p, const T* R, const T* h, E& emit) {
   T d[3] = {c[0] - p[0], c[1] - p[1], c[2] - p[2]};
   T pl[3];
   mattvec3(R, d, pl);
   T q[3];
   bool inside = true;
+#pragma unroll
   for (int k = 0; k < 3; k++) {
     q[k] = pl[k] < -h[k] ? -h[k] : (pl[k] > h[k] ? h[k] : pl[k]);
     if (q[k] != pl[k]) inside = false;
@@ -223,218 +258,498 @@ __device__ int np_sphere_box(const T* c, T r, const T* p, const T* R, const T* h
     T dl[3] = {q[0] - pl[0], q[1] - pl[1], q[2] - pl[2]};
     T len = sqrt(dot3(dl, dl));
     dist = len - r;
-    if (dist > T(0)) return 0;
+    if (dist > T(0)) return;
     for (int k = 0; k < 3; k++) nl[k] = dl[k] / len;
   } else {
+    T a0 = h[0] - fabs(pl[0]), a1 = h[1] - fabs(pl[1]), a2 = h[2] - fabs(pl[2]);
     int best = 0;
-    T bd = h[0] - fabs(pl[0]);
-    for (int k = 1; k < 3; k++) {
-      T dk = h[k] - fabs(pl[k]);
-      if (dk < bd) {
-        bd = dk;
-        best = k;
-      }
+    T bd = a0;
+    if (a1 < bd) {
+      bd = a1;
+      best = 1;
     }
-    nl[0] = nl[1] = nl[2] = 0;
-    nl[best] = pl[best] >= T(0) ? T(-1) : T(1);
+    if (a2 < bd) {
+      bd = a2;
+      best = 2;
+    }
+    T pb = best == 0 ? pl[0] : (best == 1 ? pl[1] : pl[2]);
+    T sg = pb >= T(0) ? T(-1) : T(1);
+    nl[0] = best == 0 ? sg : T(0);
+    nl[1] = best == 1 ? sg : T(0);
+    nl[2] = best == 2 ? sg : T(0);
     dist = -bd - r;
   }
   T n[3];
   matvec3(R, nl, n);
-  out[0].dist = dist;
-  for (int k = 0; k < 3; k++) {
-    out[0].n[k] = n[k];
-    out[0].pos[k] = c[k] + n[k] * (r + dist / T(2));
-  }
-  return 1;
+  T s = r + dist / T(2);
+  emit(dist, c[0] + n[0] * s, c[1] + n[1] * s, c[2] + n[2] * s, n[0], n[1], n[2]);
 }
 
+// small register-resident 3-vectors (all selections by runtime index go through selects, never
+// through indexed arrays, so nothing lands in scratch)
 template <typename T>
-__device__ int np_box_box(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2, const T* h2,
-                          Con<T>* out) {
-  T a[3][3], b[3][3];
-  for (int k = 0; k < 3; k++)
-    for (int r = 0; r < 3; r++) {
-      a[k][r] = R1[3 * r + k];
-      b[k][r] = R2[3 * r + k];
-    }
-  T d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+struct V3 {
+  T x, y, z;
+};
+template <typename T>
+__device__ __forceinline__ V3<T> vcol(const T* R, int k) {
+  return V3<T>{R[k], R[3 + k], R[6 + k]};
+}
+template <typename T>
+__device__ __forceinline__ T vdot(const V3<T>& a, const V3<T>& b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z;
+}
+template <typename T>
+__device__ __forceinline__ V3<T> vcross(const V3<T>& a, const V3<T>& b) {
+  return V3<T>{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+template <typename T>
+__device__ __forceinline__ V3<T> vsel(bool c, const V3<T>& a, const V3<T>& b) {
+  return V3<T>{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
+template <typename T>
+__device__ __forceinline__ V3<T> vpick(int i, const V3<T>& a, const V3<T>& b, const V3<T>& c) {
+  return vsel(i == 0, a, vsel(i == 1, b, c));
+}
+template <typename T>
+__device__ __forceinline__ T spick(int i, T a, T b, T c) {
+  return i == 0 ? a : (i == 1 ? b : c);
+}
+
+// box1 vs box2: SAT over 15 axes; edge-edge -> one point; face -> the vertices of the intersection of
+// the incident face with the reference face, enumerated as (1) incident vertices inside the reference
+// rectangle, (2) reference corners inside the incident quad, (3) proper edge/side crossings, each kept
+// if it penetrates (same definition as oracle/collide.c).  Normal from box1 to box2.
+template <typename T, typename E>
+__device__ __forceinline__ void np_box_box(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2,
+                                           const T* h2, E& emit) {
+  const V3<T> A[3] = {vcol(R1, 0), vcol(R1, 1), vcol(R1, 2)};
+  const V3<T> B[3] = {vcol(R2, 0), vcol(R2, 1), vcol(R2, 2)};
+  const V3<T> P1{p1[0], p1[1], p1[2]}, P2{p2[0], p2[1], p2[2]};
+  const V3<T> d{P2.x - P1.x, P2.y - P1.y, P2.z - P1.z};
   T best_face = T(1e30), best_edge = T(1e30);
   int face_id = -1, edge_id = -1;
-  T face_u[3] = {0, 0, 0}, edge_u[3] = {0, 0, 0};
+  V3<T> face_u{0, 0, 0}, edge_u{0, 0, 0};
   T face_s = 0, edge_s = 0;
+#pragma unroll
   for (int ax = 0; ax < 15; ax++) {
-    T u[3];
+    V3<T> u;
     if (ax < 3) {
-      u[0] = a[ax][0];
-      u[1] = a[ax][1];
-      u[2] = a[ax][2];
+      u = A[ax];
     } else if (ax < 6) {
-      u[0] = b[ax - 3][0];
-      u[1] = b[ax - 3][1];
-      u[2] = b[ax - 3][2];
+      u = B[ax - 3];
     } else {
-      int i = (ax - 6) / 3, j = (ax - 6) % 3;
-      cross3(a[i], b[j], u);
-      T n = sqrt(dot3(u, u));
+      u = vcross(A[(ax - 6) / 3], B[(ax - 6) % 3]);
+      T n = sqrt(vdot(u, u));
       if (n < T(1e-6)) continue;
-      for (int k = 0; k < 3; k++) u[k] /= n;
+      u = V3<T>{u.x / n, u.y / n, u.z / n};
     }
-    T ra = 0, rb = 0;
-    for (int k = 0; k < 3; k++) {
-      ra += h1[k] * fabs(dot3(u, a[k]));
-      rb += h2[k] * fabs(dot3(u, b[k]));
-    }
-    T s = dot3(u, d);
-    T ov = ra + rb - fabs(s);
-    if (ov < T(0)) return 0;
+    T ra = h1[0] * fabs(vdot(u, A[0])) + h1[1] * fabs(vdot(u, A[1])) + h1[2] * fabs(vdot(u, A[2]));
+    T rb = h2[0] * fabs(vdot(u, B[0])) + h2[1] * fabs(vdot(u, B[1])) + h2[2] * fabs(vdot(u, B[2]));
+    T sd = vdot(u, d);
+    T ov = ra + rb - fabs(sd);
+    if (ov < T(0)) return;
     if (ax < 6) {
       if (ov < best_face) {
         best_face = ov;
         face_id = ax;
-        face_u[0] = u[0];
-        face_u[1] = u[1];
-        face_u[2] = u[2];
-        face_s = s;
+        face_u = u;
+        face_s = sd;
       }
     } else if (ov < best_edge) {
       best_edge = ov;
       edge_id = ax;
-      edge_u[0] = u[0];
-      edge_u[1] = u[1];
-      edge_u[2] = u[2];
-      edge_s = s;
+      edge_u = u;
+      edge_s = sd;
     }
   }
   if (edge_id >= 0 && best_edge < T(0.95) * best_face) {
     T sg = edge_s >= T(0) ? T(1) : T(-1);
-    T n[3] = {edge_u[0] * sg, edge_u[1] * sg, edge_u[2] * sg};
-    int i = (edge_id - 6) / 3, j = (edge_id - 6) % 3;
-    T e1[3] = {p1[0], p1[1], p1[2]}, e2[3] = {p2[0], p2[1], p2[2]};
+    V3<T> n{edge_u.x * sg, edge_u.y * sg, edge_u.z * sg};
+    const int i = (edge_id - 6) / 3, j = (edge_id - 6) % 3;
+    V3<T> e1 = P1, e2 = P2;
+#pragma unroll
     for (int k = 0; k < 3; k++) {
-      if (k != i) {
-        T sgn = dot3(n, a[k]) >= T(0) ? T(1) : T(-1);
-        for (int r = 0; r < 3; r++) e1[r] += h1[k] * sgn * a[k][r];
-      }
-      if (k != j) {
-        T sgn = dot3(n, b[k]) >= T(0) ? T(-1) : T(1);
-        for (int r = 0; r < 3; r++) e2[r] += h2[k] * sgn * b[k][r];
-      }
+      T s1 = k == i ? T(0) : (vdot(n, A[k]) >= T(0) ? h1[k] : -h1[k]);
+      T s2 = k == j ? T(0) : (vdot(n, B[k]) >= T(0) ? -h2[k] : h2[k]);
+      e1 = V3<T>{e1.x + s1 * A[k].x, e1.y + s1 * A[k].y, e1.z + s1 * A[k].z};
+      e2 = V3<T>{e2.x + s2 * B[k].x, e2.y + s2 * B[k].y, e2.z + s2 * B[k].z};
     }
-    T w[3] = {e1[0] - e2[0], e1[1] - e2[1], e1[2] - e2[2]};
-    T bb = dot3(a[i], b[j]), dd = dot3(a[i], w), ee = dot3(b[j], w);
-    T den = T(1) - bb * bb;
+    const V3<T> ai = vpick(i, A[0], A[1], A[2]), bj = vpick(j, B[0], B[1], B[2]);
+    const V3<T> wv{e1.x - e2.x, e1.y - e2.y, e1.z - e2.z};
+    T bbv = vdot(ai, bj), dd = vdot(ai, wv), ee = vdot(bj, wv);
+    T den = T(1) - bbv * bbv;
     T s = 0, t = 0;
     if (den > T(1e-12)) {
-      s = (bb * ee - dd) / den;
-      t = (ee - bb * dd) / den;
+      s = (bbv * ee - dd) / den;
+      t = (ee - bbv * dd) / den;
     }
-    s = s < -h1[i] ? -h1[i] : (s > h1[i] ? h1[i] : s);
-    t = t < -h2[j] ? -h2[j] : (t > h2[j] ? h2[j] : t);
-    out[0].dist = -best_edge;
-    for (int r = 0; r < 3; r++) {
-      out[0].n[r] = n[r];
-      out[0].pos[r] = T(0.5) * (e1[r] + s * a[i][r] + e2[r] + t * b[j][r]);
-    }
-    return 1;
+    T hi_ = spick(i, h1[0], h1[1], h1[2]);
+    T hj_ = spick(j, h2[0], h2[1], h2[2]);
+    s = s < -hi_ ? -hi_ : (s > hi_ ? hi_ : s);
+    t = t < -hj_ ? -hj_ : (t > hj_ ? hj_ : t);
+    emit(-best_edge, T(0.5) * (e1.x + s * ai.x + e2.x + t * bj.x), T(0.5) * (e1.y + s * ai.y + e2.y + t * bj.y),
+         T(0.5) * (e1.z + s * ai.z + e2.z + t * bj.z), n.x, n.y, n.z);
+    return;
   }
-  T sg = face_s >= T(0) ? T(1) : T(-1);
-  T n[3] = {face_u[0] * sg, face_u[1] * sg, face_u[2] * sg};
-  const T *pr, *hr, *pi, *hi;
-  T nref[3];
-  int kr;
-  bool ref1 = face_id < 3;
-  if (ref1) {
-    pr = p1;
-    hr = h1;
-    pi = p2;
-    hi = h2;
-    kr = face_id;
-    nref[0] = n[0];
-    nref[1] = n[1];
-    nref[2] = n[2];
-  } else {
-    pr = p2;
-    hr = h2;
-    pi = p1;
-    hi = h1;
-    kr = face_id - 3;
-    nref[0] = -n[0];
-    nref[1] = -n[1];
-    nref[2] = -n[2];
-  }
-  T(*ar)[3] = ref1 ? a : b;
-  T(*ai)[3] = ref1 ? b : a;
-  T fc[3];
-  for (int k = 0; k < 3; k++) fc[k] = pr[k] + nref[k] * hr[kr];
-  int t1 = (kr + 1) % 3, t2 = (kr + 2) % 3;
+  // ---- face contact: reference box (owner of the face axis) and incident box
+  const T sg = face_s >= T(0) ? T(1) : T(-1);
+  const V3<T> n{face_u.x * sg, face_u.y * sg, face_u.z * sg};
+  const bool ref1 = face_id < 3;
+  const int kr = ref1 ? face_id : face_id - 3;
+  const V3<T> Rr0 = vsel(ref1, A[0], B[0]), Rr1 = vsel(ref1, A[1], B[1]), Rr2 = vsel(ref1, A[2], B[2]);
+  const V3<T> Ri0 = vsel(ref1, B[0], A[0]), Ri1 = vsel(ref1, B[1], A[1]), Ri2 = vsel(ref1, B[2], A[2]);
+  const T hr0 = ref1 ? h1[0] : h2[0], hr1 = ref1 ? h1[1] : h2[1], hr2 = ref1 ? h1[2] : h2[2];
+  const T hi0 = ref1 ? h2[0] : h1[0], hi1 = ref1 ? h2[1] : h1[1], hi2 = ref1 ? h2[2] : h1[2];
+  const V3<T> pr = vsel(ref1, P1, P2), pi = vsel(ref1, P2, P1);
+  const V3<T> nref = ref1 ? n : V3<T>{-n.x, -n.y, -n.z};
+  const int t1 = (kr + 1) % 3, t2 = (kr + 2) % 3;
+  const T hrk = spick(kr, hr0, hr1, hr2);
+  const V3<T> fc{pr.x + nref.x * hrk, pr.y + nref.y * hrk, pr.z + nref.z * hrk};
+  const V3<T> ta = vpick(t1, Rr0, Rr1, Rr2), tb = vpick(t2, Rr0, Rr1, Rr2);
+  const T e1 = spick(t1, hr0, hr1, hr2), e2 = spick(t2, hr0, hr1, hr2);
+  // incident face: the incident box axis most anti-parallel to nref
+  const T dk0 = vdot(nref, Ri0), dk1 = vdot(nref, Ri1), dk2 = vdot(nref, Ri2);
   int mi = 0;
-  T bestdot = T(-1);
-  for (int k = 0; k < 3; k++) {
-    T dk = fabs(dot3(nref, ai[k]));
-    if (dk > bestdot) {
-      bestdot = dk;
-      mi = k;
-    }
+  T bestdot = fabs(dk0), dmi = dk0;
+  if (fabs(dk1) > bestdot) {
+    bestdot = fabs(dk1);
+    mi = 1;
+    dmi = dk1;
   }
-  T sgn = dot3(nref, ai[mi]) > T(0) ? T(-1) : T(1);
-  T ic[3];
-  for (int k = 0; k < 3; k++) ic[k] = pi[k] + sgn * hi[mi] * ai[mi][k];
-  int u1 = (mi + 1) % 3, u2 = (mi + 2) % 3;
-  T poly[8][3], tmp[8][3];
+  if (fabs(dk2) > bestdot) {
+    mi = 2;
+    dmi = dk2;
+  }
+  const T sgn = dmi > T(0) ? T(-1) : T(1);
+  const int u1 = (mi + 1) % 3, u2 = (mi + 2) % 3;
+  const T him = spick(mi, hi0, hi1, hi2), hu1 = spick(u1, hi0, hi1, hi2), hu2 = spick(u2, hi0, hi1, hi2);
+  const V3<T> am = vpick(mi, Ri0, Ri1, Ri2), a1 = vpick(u1, Ri0, Ri1, Ri2), a2 = vpick(u2, Ri0, Ri1, Ri2);
+  // incident face centre relative to the reference face centre, in reference coordinates (u, v, w)
+  const V3<T> icr{pi.x + sgn * him * am.x - fc.x, pi.y + sgn * him * am.y - fc.y, pi.z + sgn * him * am.z - fc.z};
+  const T cu = vdot(icr, ta), cv = vdot(icr, tb), cw = vdot(icr, nref);
+  const T a1u = hu1 * vdot(a1, ta), a1v = hu1 * vdot(a1, tb), a1w = hu1 * vdot(a1, nref);
+  const T a2u = hu2 * vdot(a2, ta), a2v = hu2 * vdot(a2, tb), a2w = hu2 * vdot(a2, nref);
   const T sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
-  for (int vtx = 0; vtx < 4; vtx++)
-    for (int k = 0; k < 3; k++)
-      poly[vtx][k] = ic[k] + sx[vtx] * hi[u1] * ai[u1][k] + sy[vtx] * hi[u2] * ai[u2][k];
-  int np = 4;
-  for (int pl = 0; pl < 4 && np > 0; pl++) {
-    const T* t = ar[pl < 2 ? t1 : t2];
-    T e = hr[pl < 2 ? t1 : t2];
-    T sside = (pl & 1) ? T(-1) : T(1);
-    int nn = 0;
-    for (int vtx = 0; vtx < np; vtx++) {
-      const T* P = poly[vtx];
-      const T* Q = poly[(vtx + 1) % np];
-      T rp[3] = {P[0] - fc[0], P[1] - fc[1], P[2] - fc[2]};
-      T rq[3] = {Q[0] - fc[0], Q[1] - fc[1], Q[2] - fc[2]};
-      T dp = e - sside * dot3(rp, t);
-      T dq = e - sside * dot3(rq, t);
-      if (dp >= T(0) && nn < 8) {
-        tmp[nn][0] = P[0];
-        tmp[nn][1] = P[1];
-        tmp[nn][2] = P[2];
-        nn++;
-      }
-      if ((dp >= T(0)) != (dq >= T(0)) && nn < 8) {
-        T f = dp / (dp - dq);
-        for (int k = 0; k < 3; k++) tmp[nn][k] = P[k] + (Q[k] - P[k]) * f;
-        nn++;
+  T U[4], V[4], W[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    U[k] = cu + sx[k] * a1u + sy[k] * a2u;
+    V[k] = cv + sx[k] * a1v + sy[k] * a2v;
+    W[k] = cw + sx[k] * a1w + sy[k] * a2w;
+  }
+  auto out = [&](T u, T v, T w) {
+    if (w > T(0)) return;  // not penetrating
+    T hw = T(0.5) * w;
+    emit(w, fc.x + u * ta.x + v * tb.x + hw * nref.x, fc.y + u * ta.y + v * tb.y + hw * nref.y,
+         fc.z + u * ta.z + v * tb.z + hw * nref.z, n.x, n.y, n.z);
+  };
+  // (1) incident vertices inside the reference rectangle
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (fabs(U[k]) <= e1 && fabs(V[k]) <= e2) out(U[k], V[k], W[k]);
+  // (2) reference corners inside the incident quad (projected along nref), w on the incident plane
+  const T det = a1u * a2v - a2u * a1v;
+  const T ia = a1w * a2v - a2w * a1v, ib = a1u * a2w - a2u * a1w;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const T cu_ = sx[k] * e1, cv_ = sy[k] * e2;
+    bool in = det != T(0);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int m1 = (m + 1) & 3;
+      T cr = (U[m1] - U[m]) * (cv_ - V[m]) - (V[m1] - V[m]) * (cu_ - U[m]);
+      in = in && (det >= T(0) ? cr > T(0) : cr < T(0));
+    }
+    if (in) out(cu_, cv_, cw + (ia * (cu_ - cu) + ib * (cv_ - cv)) / det);
+  }
+  // (3) proper crossings of incident edges with the rectangle's sides
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int m1 = (m + 1) & 3;
+#pragma unroll
+    for (int sd = 0; sd < 4; sd++) {
+      const bool onu = sd < 2;
+      const T ss = (sd & 1) ? T(-1) : T(1);
+      const T e = onu ? e1 : e2;
+      const T dp = e - ss * (onu ? U[m] : V[m]);
+      const T dq = e - ss * (onu ? U[m1] : V[m1]);
+      if ((dp > T(0) && dq < T(0)) || (dp < T(0) && dq > T(0))) {
+        const T f = dp / (dp - dq);
+        const T xu = U[m] + (U[m1] - U[m]) * f, xv = V[m] + (V[m1] - V[m]) * f, xw = W[m] + (W[m1] - W[m]) * f;
+        if (onu ? fabs(xv) <= e2 : fabs(xu) < e1) out(xu, xv, xw);
       }
     }
-    np = nn;
-    for (int vtx = 0; vtx < nn; vtx++)
-      for (int k = 0; k < 3; k++) poly[vtx][k] = tmp[vtx][k];
   }
-  int cnt = 0;
-  for (int vtx = 0; vtx < np && cnt < 8; vtx++) {
-    T rv[3] = {fc[0] - poly[vtx][0], fc[1] - poly[vtx][1], fc[2] - poly[vtx][2]};
-    T depth = dot3(rv, nref);
-    if (depth < T(0)) continue;
-    out[cnt].dist = -depth;
-    for (int k = 0; k < 3; k++) {
-      out[cnt].n[k] = n[k];
-      out[cnt].pos[k] = poly[vtx][k] + nref[k] * depth / T(2);
+}
+
+// ------------------------------------------------------------------------------------------------
+// collision (mj_collision): two-level broadphase + narrowphase
+//   1. world centres of the moving geoms (gx[g] = centre, rbound)
+//   2. bounds of the collision bodies (moving bodies: sphere about the body origin; static groups and
+//      the belt: AABBs; the floor: half-space) and a test of every body pair MuJoCo's filters allow
+//   3. expansion of the surviving body pairs into geom pairs + MuJoCo's bounding-sphere test
+//   4. narrowphase per geom pair (one pair per lane), contacts staged with LDS atomics
+//   5. staged contacts sorted by (geom pair, index) into the contact slots
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void geom_frame(const Model<T>& M, const Ws<T>& w, int g, int kb, T* R, T* h) {
+  const Dims& dm = M.dm;
+  const T* gg = M.geom + 16 * g;
+  if (kb >= 2 && kb < 2 + dm.K) {
+    const T* c = w.cR() + 9 * (kb - 2);
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = c[k];
+    T hh = w.cube()[4 * (kb - 2)];
+    h[0] = h[1] = h[2] = hh;
+    return;
+  }
+  h[0] = gg[12];
+  h[1] = gg[13];
+  h[2] = gg[14];
+  if (kb == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = gg[3 + k];
+  } else if (kb == 1) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? T(1) : T(0);
+  } else {
+    int arm = (kb - 2 - dm.K) / 10, b = (kb - 2 - dm.K) % 10;
+    matmul3(w.bR() + 90 * arm + 9 * b, gg + 3, R);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T>& w, const uint32_t* list, int n) {
+  const Dims& dm = M.dm;
+  if (LANE >= n) return;
+  uint32_t pwd = list[LANE];
+  int c1 = pwd & 4095, c2 = (pwd >> 12) & 4095;
+  const int gi1 = w.ginfo()[c1], gi2 = w.ginfo()[c2];
+  const int t1 = gi1 & 3, t2 = gi2 & 3;
+  const int kb1 = (gi1 >> 8) & 255, kb2 = (gi2 >> 8) & 255;
+  const T* x1 = w.gx() + 4 * c1;
+  const T* x2 = w.gx() + 4 * c2;
+  int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
+  Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
+  T p1[3] = {x1[0], x1[1], x1[2]}, p2[3] = {x2[0], x2[1], x2[2]};
+  if (t1 == GC_PLANE) {
+    if (t2 == GC_SPHERE) {
+      np_plane_sphere(p2, x2[3], emit);
+    } else {
+      T R[9], h[3];
+      geom_frame(M, w, c2, kb2, R, h);
+      np_plane_box(p2, R, h, emit);
     }
-    cnt++;
+  } else if (t1 == GC_SPHERE) {
+    if (t2 == GC_SPHERE) {
+      np_sphere_sphere(p1, x1[3], p2, x2[3], emit);
+    } else {
+      T R[9], h[3];
+      geom_frame(M, w, c2, kb2, R, h);
+      np_sphere_box(p1, x1[3], p2, R, h, emit);
+    }
+  } else {
+    T Ra[9], ha[3], Rb[9], hb[3];
+    geom_frame(M, w, c1, kb1, Ra, ha);
+    geom_frame(M, w, c2, kb2, Rb, hb);
+    np_box_box(p1, Ra, ha, p2, Rb, hb, emit);
   }
-  return cnt;
+}
+
+template <typename T>
+__device__ __forceinline__ void collide(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
+  const Dims& dm = M.dm;
+  const int K = dm.K;
+  const T* q = w.q();
+  T* gx = w.gx();
+  const int* gin = w.ginfo();
+  const int* cbi = w.cbi();
+  int* misc = w.misc();
+  const uint64_t below = (1ull << LANE) - 1ull;
+  // 1. moving geom centres (static ones were written at launch)
+  for (int g = LANE; g < dm.ngc; g += WAVE) {
+    int kb = (gin[g] >> 8) & 255;
+    if (kb == 0) continue;
+    T* o = gx + 4 * g;
+    if (kb == 1) {
+      o[0] = 0;
+      o[1] = q[0];
+      o[2] = T(1.05);
+    } else if (kb < 2 + K) {
+      const T* c = q + 1 + 7 * (kb - 2);
+      o[0] = c[0];
+      o[1] = c[1];
+      o[2] = c[2];
+    } else {
+      int arm = (kb - 2 - K) / 10, b = (kb - 2 - K) % 10;
+      const T* gg = M.geom + 16 * g;
+      const T* bp = w.bpos() + 30 * arm + 3 * b;
+      const T* bR = w.bR() + 90 * arm + 9 * b;
+      T off[3];
+      matvec3(bR, gg, off);
+      o[0] = bp[0] + off[0];
+      o[1] = bp[1] + off[1];
+      o[2] = bp[2] + off[2];
+    }
+  }
+  // 2. collision-body bounds
+  for (int b = LANE; b < dm.ncb; b += WAVE) {
+    const int kb = cbi[4 * b], fl = cbi[4 * b + 1];
+    if (fl & CB_STATIC) continue;
+    T* o = w.cbw() + 8 * b;
+    if (kb == 1) {
+      o[1] = q[0];
+    } else if (kb < 2 + K) {
+      const T* c = q + 1 + 7 * (kb - 2);
+      o[0] = c[0];
+      o[1] = c[1];
+      o[2] = c[2];
+    } else {
+      const T* bp = w.bpos() + 30 * ((kb - 2 - K) / 10) + 3 * ((kb - 2 - K) % 10);
+      o[0] = bp[0];
+      o[1] = bp[1];
+      o[2] = bp[2];
+    }
+  }
+  if (LANE == 0) misc[MISC_NSTAGE] = 0;
+  SYNC();
+  uint32_t* sp = w.sp();
+  int* spoff = w.spoff();
+  uint32_t* gs = w.gsurv();
+  int nsurv = 0;
+  for (int p0 = 0; p0 < dm.ncbp; p0 += WAVE) {
+    const int pidx = p0 + LANE;
+    bool hit = false;
+    int ncomb = 0;
+    uint32_t bpw = 0;
+    if (pidx < dm.ncbp) {
+      bpw = M.cbp[pidx];
+      const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
+      const T* X = w.cbw() + 8 * b1;
+      const T* Y = w.cbw() + 8 * b2;
+      const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1];
+      if (f1 & CB_PLANE) {
+        hit = Y[2] - Y[6] - Y[3] <= T(0);
+      } else if (f2 & CB_PLANE) {
+        hit = X[2] - X[6] - X[3] <= T(0);
+      } else {
+        T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
+        T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
+        T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
+        d0 = d0 > T(0) ? d0 : T(0);
+        d1 = d1 > T(0) ? d1 : T(0);
+        d2 = d2 > T(0) ? d2 : T(0);
+        T rr = X[3] + Y[3];
+        hit = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
+      }
+      if (hit) ncomb = cbi[4 * b1 + 3] * cbi[4 * b2 + 3];
+    }
+    const uint64_t bal = __ballot(hit);
+    const int nsp = __popcll(bal);
+    int incl = ncomb;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+      int y = __shfl_up(incl, o);
+      if (LANE >= o) incl += y;
+    }
+    const int total = __shfl(incl, WAVE - 1);
+    if (hit) {
+      int slot = __popcll(bal & below);
+      sp[slot] = bpw;
+      spoff[slot] = incl - ncomb;
+    }
+    SYNC();
+    for (int e0 = 0; e0 < total; e0 += WAVE) {
+      const int e = e0 + LANE;
+      bool ok = false;
+      uint32_t pk = 0;
+      if (e < total) {
+        int lo = 0, hi = nsp - 1;
+        while (lo < hi) {
+          int mid = (lo + hi + 1) >> 1;
+          if (spoff[mid] <= e)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        const uint32_t bp = sp[lo];
+        const int x = bp & 255, y = (bp >> 8) & 255;
+        const int r = e - spoff[lo];
+        const int ngy = cbi[4 * y + 3];
+        const int i = r / ngy, j = r - i * ngy;
+        int ga = w.cbg()[cbi[4 * x + 2] + i], gb = w.cbg()[cbi[4 * y + 2] + j];
+        const T* xa = gx + 4 * ga;
+        const T* xb = gx + 4 * gb;
+        ok = true;
+        if (xa[3] > T(0) && xb[3] > T(0)) {
+          T d0 = xa[0] - xb[0], d1 = xa[1] - xb[1], d2 = xa[2] - xb[2];
+          T rs = xa[3] + xb[3];
+          ok = sqrt(d0 * d0 + d1 * d1 + d2 * d2) <= rs;
+        }
+        if (ok) {
+          int c1 = ga < gb ? ga : gb, c2 = ga < gb ? gb : ga;
+          if ((gin[c1] & 3) > (gin[c2] & 3)) {
+            int t = c1;
+            c1 = c2;
+            c2 = t;
+          }
+          int pc = 5 * ((gin[c1] >> GI_PC) & 7) + ((gin[c2] >> GI_PC) & 7);
+          pk = (uint32_t)c1 | ((uint32_t)c2 << 12) | ((uint32_t)M.ptab[pc] << 24);
+        }
+      }
+      const uint64_t b2m = __ballot(ok);
+      if (ok) gs[nsurv + __popcll(b2m & below)] = pk;
+      nsurv += __popcll(b2m);
+      SYNC();
+      if (nsurv >= WAVE) {
+        narrow_batch(M, w, gs, WAVE);
+        const bool mv = LANE + WAVE < nsurv;
+        uint32_t t = mv ? gs[LANE + WAVE] : 0u;
+        SYNC();
+        if (mv) gs[LANE] = t;
+        nsurv -= WAVE;
+        SYNC();
+      }
+    }
+    SYNC();
+  }
+  if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
+  SYNC();
+  // 5. sort the staged contacts by key into the contact slots
+  const int nst = misc[MISC_NSTAGE];
+  const int ncon = nst < dm.maxcon ? nst : dm.maxcon;
+  if (LANE == 0 && nst > dm.maxcon) ctr[0] += nst - dm.maxcon;
+  for (int s = LANE; s < ncon; s += WAVE) {
+    const int key = w.skey()[s];
+    int rank = 0;
+    for (int t = 0; t < ncon; t++) rank += w.skey()[t] < key ? 1 : 0;
+    const T* st = w.stage() + 8 * s;
+    int* ci = w.ci() + 4 * rank;
+    T* cr = w.cr() + CR_N * rank;
+    const uint32_t pwd = w.spw()[s];
+    ci[0] = (int)(pwd & 0xFFFFFF);
+    ci[3] = (int)(pwd >> 24);
+    cr[CR_DIST] = st[0];
+    cr[CR_POS] = st[1];
+    cr[CR_POS + 1] = st[2];
+    cr[CR_POS + 2] = st[3];
+    cr[CR_FR] = st[4];
+    cr[CR_FR + 1] = st[5];
+    cr[CR_FR + 2] = st[6];
+  }
+  if (LANE == 0) {
+    misc[MISC_NCON] = ncon;
+    misc[MISC_NROW] = 0;
+  }
+  SYNC();
 }
 
 // ------------------------------------------------------------------------------------------------
 // stage (mj_step1): kinematics, inertia, bias forces, collision, constraint rows, efc velocities
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__device__ void arm_chain(const Model<T>& M, const Ws<T>& w, int arm, bool with_dyn) {
+__device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T>& w, int arm, bool with_dyn) {
   const Dims& dm = M.dm;
   const T* q = w.q() + 1 + 7 * dm.K + 9 * arm;
   const T* qd = w.v() + 1 + 6 * dm.K + 9 * arm;
@@ -644,7 +959,7 @@ __device__ __forceinline__ void arm_jac_col(const Ws<T>& w, int arm, int b, int 
 
 // translational Jacobian column j (tree-local) of point p on kernel body kb in its tree
 template <typename T>
-__device__ void body_jac_col(const Model<T>& M, const Ws<T>& w, int kb, int j, const T* p, T* col) {
+__device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T>& w, int kb, int j, const T* p, T* col) {
   const Dims& dm = M.dm;
   if (kb == 1) {
     col[0] = 0;
@@ -669,7 +984,7 @@ __device__ void body_jac_col(const Model<T>& M, const Ws<T>& w, int kb, int j, c
 }
 
 template <typename T>
-__device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
+__device__ __forceinline__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
   const Dims& dm = M.dm;
   const int A = dm.A, K = dm.K, nv = dm.nv;
   T* q = w.q();
@@ -699,7 +1014,7 @@ __device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr
     R[8] = ww * ww - x * x - y * y + z * z;
     // passive - bias of the free joint: gravity only (com at the body origin, isotropic inertia)
     T* pb = w.pb() + 1 + 6 * k;
-    T m = M.cube[((size_t)arena * K + k) * 4 + 1];
+    T m = w.cube()[4 * k + 1];
     pb[0] = 0;
     pb[1] = 0;
     pb[2] = -m * M.grav;
@@ -707,6 +1022,7 @@ __device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr
   }
   if (LANE == 0) w.pb()[0] = -M.belt_damp * v[0];  // belt: damping, no gravity along y
   SYNC();
+  PMARK(PH_FK);
   // ---- actuator length / velocity (transmission at the stage state)
   for (int u = LANE; u < dm.nu; u += WAVE) {
     T L, V;
@@ -726,34 +1042,6 @@ __device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr
     }
     w.alen()[u] = L;
     w.avel()[u] = V;
-  }
-  // ---- geom world poses of moving geoms
-  for (int g = LANE; g < dm.ngc; g += WAVE) {
-    const int* gi = M.geom_i + 4 * g;
-    int kb = gi[2], slot = gi[3];
-    if (kb == 0) continue;
-    const T* gg = M.geom + 16 * g;
-    T* gx = w.gx() + 3 * g;
-    if (kb == 1) {
-      gx[0] = 0;
-      gx[1] = q[0];
-      gx[2] = T(1.05);
-      T* R = w.gR() + 9 * slot;
-      for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? T(1) : T(0);
-    } else if (kb < 2 + K) {
-      int k = kb - 2;
-      for (int c = 0; c < 3; c++) gx[c] = q[1 + 7 * k + c];
-      T* R = w.gR() + 9 * slot;
-      for (int c = 0; c < 9; c++) R[c] = w.cR()[9 * k + c];
-    } else {
-      int arm = (kb - 2 - K) / 10, b = (kb - 2 - K) % 10;
-      const T* bp = w.bpos() + 30 * arm + 3 * b;
-      const T* bR = w.bR() + 90 * arm + 9 * b;
-      T off[3];
-      matvec3(bR, gg, off);
-      for (int c = 0; c < 3; c++) gx[c] = bp[c] + off[c];
-      if (slot >= 0) matmul3(bR, gg + 3, w.gR() + 9 * slot);
-    }
   }
   // ---- arm mass-matrix blocks: M_ij = sum_{b in desc} m Jc_i.Jc_j + Jr_i' Iw Jr_j
   for (int e = LANE; e < 45 * A; e += WAVE) {
@@ -793,137 +1081,22 @@ __device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr
     Ma[9 * i + j] = s;
     Ma[9 * j + i] = s;
   }
-  // ---- broadphase (bounding spheres) + narrowphase, in chunks of MAXSURV survivors
+  PMARK(PH_GEOM);
+  collide(M, w, arena, ctr);
   int* misc = w.misc();
-  if (LANE == 0) {
-    misc[MISC_NCON] = 0;
-    misc[MISC_NROW] = 0;
-  }
-  SYNC();
-  int start = 0;
-  while (start < dm.npair) {
-    int nsurv = 0;
-    int p = start;
-    for (; p < dm.npair && nsurv + WAVE <= MAXSURV; p += WAVE) {
-      int idx = p + LANE;
-      bool hit = false;
-      if (idx < dm.npair) {
-        uint32_t pw = M.pair[idx];
-        int c1 = pw & 4095, c2 = (pw >> 12) & 4095;
-        T r1 = M.geom[16 * c1 + 15], r2 = M.geom[16 * c2 + 15];
-        if (r1 > T(0) && r2 > T(0)) {
-          const T* x1 = w.gx() + 3 * c1;
-          const T* x2 = w.gx() + 3 * c2;
-          T d0 = x1[0] - x2[0], d1 = x1[1] - x2[1], d2 = x1[2] - x2[2];
-          T rs = r1 + r2;
-          hit = sqrt(d0 * d0 + d1 * d1 + d2 * d2) <= rs;
-        } else {
-          hit = true;  // planes: no bounding test (MuJoCo)
-        }
-      }
-      uint64_t bal = __ballot(hit);
-      int before = __popcll(bal & ((1ull << LANE) - 1ull));
-      if (hit) w.surv()[nsurv + before] = (uint16_t)idx;
-      nsurv += __popcll(bal);
-    }
-    start = p;
-    SYNC();
-    // narrowphase: one survivor pair per lane, contacts appended in pair order (wave prefix sum)
-    for (int s0 = 0; s0 < nsurv; s0 += WAVE) {
-      int sidx = s0 + LANE;
-      Con<T> cs[MAXPC];
-      int nc = 0;
-      int c1 = 0, c2 = 0;
-      if (sidx < nsurv) {
-        uint32_t pw = M.pair[w.surv()[sidx]];
-        c1 = pw & 4095;
-        c2 = (pw >> 12) & 4095;
-        int t1 = M.geom_i[4 * c1 + 1], t2 = M.geom_i[4 * c2 + 1];
-        const T* x1 = w.gx() + 3 * c1;
-        const T* x2 = w.gx() + 3 * c2;
-        if (t1 == GT_PLANE && t2 == GT_SPHERE) {
-          nc = np_plane_sphere(x2, M.geom[16 * c2 + 12], cs);
-        } else if (t1 == GT_PLANE && t2 == GT_BOX) {
-          T h[3];
-          if (M.geom_i[4 * c2 + 2] >= 2 && M.geom_i[4 * c2 + 2] < 2 + K) {
-            T hh = M.cube[((size_t)arena * K + (M.geom_i[4 * c2 + 2] - 2)) * 4];
-            h[0] = h[1] = h[2] = hh;
-          } else {
-            for (int k = 0; k < 3; k++) h[k] = M.geom[16 * c2 + 12 + k];
-          }
-          nc = np_plane_box(x2, w.gR() + 9 * M.geom_i[4 * c2 + 3], h, cs);
-        } else if (t1 == GT_SPHERE && t2 == GT_SPHERE) {
-          nc = np_sphere_sphere(x1, M.geom[16 * c1 + 12], x2, M.geom[16 * c2 + 12], cs);
-        } else if (t1 == GT_SPHERE && t2 == GT_BOX) {
-          T h[3];
-          if (M.geom_i[4 * c2 + 2] >= 2 && M.geom_i[4 * c2 + 2] < 2 + K) {
-            T hh = M.cube[((size_t)arena * K + (M.geom_i[4 * c2 + 2] - 2)) * 4];
-            h[0] = h[1] = h[2] = hh;
-          } else {
-            for (int k = 0; k < 3; k++) h[k] = M.geom[16 * c2 + 12 + k];
-          }
-          nc = np_sphere_box(x1, M.geom[16 * c1 + 12], x2, w.gR() + 9 * M.geom_i[4 * c2 + 3], h, cs);
-        } else if (t1 == GT_BOX && t2 == GT_BOX) {
-          T h1[3], h2[3];
-          int kb1 = M.geom_i[4 * c1 + 2], kb2 = M.geom_i[4 * c2 + 2];
-          for (int k = 0; k < 3; k++) {
-            h1[k] = M.geom[16 * c1 + 12 + k];
-            h2[k] = M.geom[16 * c2 + 12 + k];
-          }
-          if (kb1 >= 2 && kb1 < 2 + K) h1[0] = h1[1] = h1[2] = M.cube[((size_t)arena * K + kb1 - 2) * 4];
-          if (kb2 >= 2 && kb2 < 2 + K) h2[0] = h2[1] = h2[2] = M.cube[((size_t)arena * K + kb2 - 2) * 4];
-          nc = np_box_box(x1, w.gR() + 9 * M.geom_i[4 * c1 + 3], h1, x2, w.gR() + 9 * M.geom_i[4 * c2 + 3], h2,
-                          cs);
-        }
-      }
-      // exclusive prefix sum of nc over the wave
-      int incl = nc;
-#pragma unroll
-      for (int o = 1; o < WAVE; o <<= 1) {
-        int y = __shfl_up(incl, o);
-        if (LANE >= o) incl += y;
-      }
-      int total = __shfl(incl, WAVE - 1);
-      int base = misc[MISC_NCON];
-      int off = base + incl - nc;
-      for (int c = 0; c < nc; c++) {
-        int slot = off + c;
-        if (slot >= dm.maxcon) break;
-        int* ci = w.ci() + 4 * slot;
-        T* cr = w.cr() + CR_N * slot;
-        uint32_t pw = M.pair[w.surv()[sidx]];
-        ci[0] = (int)(pw & 0xFFFFFF);
-        ci[3] = (int)(pw >> 24);
-        cr[CR_DIST] = cs[c].dist;
-        for (int k = 0; k < 3; k++) {
-          cr[CR_POS + k] = cs[c].pos[k];
-          cr[CR_FR + k] = cs[c].n[k];
-        }
-      }
-      SYNC();
-      if (LANE == 0) {
-        int nt = base + total;
-        if (nt > dm.maxcon) {
-          ctr[0] += nt - dm.maxcon;
-          nt = dm.maxcon;
-        }
-        misc[MISC_NCON] = nt;
-      }
-      SYNC();
-    }
-  }
-  SYNC();
+  PMARK(PH_COLL);
   const int ncon = misc[MISC_NCON];
+  if (M.prof && LANE == 0) w.prof()[PH_NCON] += ncon;
   // ---- contact rows: frame, Jacobian blocks, impedance, D, reference-acceleration terms
   for (int c = LANE; c < ncon; c += WAVE) {
     int* ci = w.ci() + 4 * c;
     T* cr = w.cr() + CR_N * c;
     int c1 = ci[0] & 4095, c2 = (ci[0] >> 12) & 4095;
     int pidx = ci[3];
-    int kb1 = M.geom_i[4 * c1 + 2], kb2 = M.geom_i[4 * c2 + 2];
+    const int gi1 = w.ginfo()[c1], gi2 = w.ginfo()[c2];
+    int kb1 = (gi1 >> 8) & 255, kb2 = (gi2 >> 8) & 255;
     int tr1 = kbody_tree(dm, kb1), tr2 = kbody_tree(dm, kb2);
-    int mj1 = M.geom_i[4 * c1], mj2 = M.geom_i[4 * c2];
-    int armflag = (mj1 >= 13 + K || mj2 >= 13 + K) ? 1 : 0;
+    int armflag = ((gi1 | gi2) >> GI_ARM) & 1;
     // frame (mju_makeFrame)
     T* f = cr + CR_FR;
     T nn = sqrt(dot3(f, f));
@@ -996,7 +1169,7 @@ __device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr
     auto invw_t = [&](int kb) -> T {
       if (kb == 0) return T(0);
       if (kb == 1) return M.belt_invw_t;
-      if (kb < 2 + K) return T(1) / M.cube[((size_t)arena * K + kb - 2) * 4 + 1];
+      if (kb < 2 + K) return T(1) / w.cube()[4 * (kb - 2) + 1];
       return M.body[32 * ((kb - 2 - K) % 10) + 28];
     };
     T tran = invw_t(kb1) + invw_t(kb2);
@@ -1064,28 +1237,28 @@ __device__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr
   }
   (void)nv;
   SYNC();
+  PMARK(PH_ROWS);
 }
 
 // ------------------------------------------------------------------------------------------------
 // block-diagonal M products and solves (belt scalar, cubes diagonal, arm 9x9 blocks)
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__device__ T Mdiag(const Model<T>& M, int arena, int i) {
-  const Dims& dm = M.dm;
+__device__ __forceinline__ T Mdiag(const Model<T>& M, const Ws<T>& w, int i) {
   if (i == 0) return M.belt_mass;
   int k = (i - 1) / 6, r = (i - 1) % 6;
-  const T* c = M.cube + ((size_t)arena * dm.K + k) * 4;
+  const T* c = w.cube() + 4 * k;
   return r < 3 ? c[1] : c[2];
 }
 
 // out = M x   (lanes over dofs)
 template <typename T>
-__device__ void mmul(const Model<T>& M, const Ws<T>& w, int arena, const T* x, T* out) {
+__device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T>& w, int arena, const T* x, T* out) {
   const Dims& dm = M.dm;
   int a0 = 1 + 6 * dm.K;
   for (int i = LANE; i < dm.nv; i += WAVE) {
     if (i < a0) {
-      out[i] = Mdiag(M, arena, i) * x[i];
+      out[i] = Mdiag(M, w, i) * x[i];
     } else {
       int arm = (i - a0) / 9, r = (i - a0) % 9;
       const T* Mb = w.Marm() + 81 * arm + 9 * r;
@@ -1099,7 +1272,7 @@ __device__ void mmul(const Model<T>& M, const Ws<T>& w, int arena, const T* x, T
 
 // in-place 9x9 Cholesky (lower), one lane
 template <typename T>
-__device__ void chol9(T* A) {
+__device__ __forceinline__ void chol9(T* A) {
   for (int j = 0; j < 9; j++) {
     T s = A[9 * j + j];
     for (int k = 0; k < j; k++) s -= A[9 * j + k] * A[9 * j + k];
@@ -1113,7 +1286,7 @@ __device__ void chol9(T* A) {
   }
 }
 template <typename T>
-__device__ void cholsolve9(const T* L, T* x) {
+__device__ __forceinline__ void cholsolve9(const T* L, T* x) {
   for (int i = 0; i < 9; i++) {
     T t = x[i];
     for (int k = 0; k < i; k++) t -= L[9 * i + k] * x[k];
@@ -1136,7 +1309,7 @@ __device__ __forceinline__ T edge_val(const T* x3, T mu, int e) {
 
 // evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
 template <typename T>
-__device__ T rows_eval(const Model<T>& M, const Ws<T>& w, const T* x, int ncon, int nrow) {
+__device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T>& w, const T* x, int ncon, int nrow) {
   const Dims& dm = M.dm;
   T cst = 0;
   for (int c = LANE; c < ncon; c += WAVE) {
@@ -1175,7 +1348,7 @@ __device__ T rows_eval(const Model<T>& M, const Ws<T>& w, const T* x, int ncon, 
 
 // f3 (per contact, stored in CR_F[0..2]) = D * sum_active jar_e c_e ; used for gradient / forces
 template <typename T>
-__device__ void contact_f3(const Ws<T>& w, int ncon) {
+__device__ __forceinline__ void contact_f3(const Ws<T>& w, int ncon) {
   for (int c = LANE; c < ncon; c += WAVE) {
     T* cr = w.cr() + CR_N * c;
     T mu = cr[CR_MU], D = cr[CR_D];
@@ -1201,7 +1374,7 @@ __device__ void contact_f3(const Ws<T>& w, int ncon) {
 
 // out_i = sum over rows of J_ri * (D jar)_r for active rows  (constraint part of the gradient)
 template <typename T>
-__device__ void gather_JtF(const Model<T>& M, const Ws<T>& w, int ncon, int nrow, T* out, bool add) {
+__device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T>& w, int ncon, int nrow, T* out, bool add) {
   const Dims& dm = M.dm;
   for (int i = LANE; i < dm.nv; i += WAVE) {
     int t = dof_tree(dm, i);
@@ -1232,7 +1405,7 @@ __device__ void gather_JtF(const Model<T>& M, const Ws<T>& w, int ncon, int nrow
 }
 
 template <typename T>
-__device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
+__device__ __forceinline__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
   const Dims& dm = M.dm;
   const int nv = dm.nv;
   const int ncon = w.misc()[MISC_NCON], nrow = w.misc()[MISC_NROW];
@@ -1266,6 +1439,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
   SYNC();
   T cost = quad(a) + rows_eval(M, w, a, ncon, nrow);
   SYNC();
+  PMARK(PH_NSETUP);
   int it;
   const int maxit = M.solver_iter;
   const int ntri = nv * (nv + 1) / 2;
@@ -1281,6 +1455,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
       gn += g[i] * g[i];
     }
     gn = wave_sum(gn);
+    PMARK(PH_NGRAD);
     if (scale * sqrt(gn) < tol) break;
     // Hessian H = M + sum_c B_c' K_c B_c + generic rows
     for (int e = LANE; e < nv * nv; e += WAVE) H[e] = T(0);
@@ -1289,7 +1464,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
       int a0 = 1 + 6 * dm.K;
       for (int i = LANE; i < nv; i += WAVE) {
         if (i < a0) {
-          H[i * nv + i] = Mdiag(M, arena, i);
+          H[i * nv + i] = Mdiag(M, w, i);
         } else {
           int arm = (i - a0) / 9, r = (i - a0) % 9;
           for (int j = 0; j < 9; j++) H[i * nv + a0 + 9 * arm + j] = w.Marm()[81 * arm + 9 * r + j];
@@ -1352,6 +1527,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
       }
     }
     SYNC();
+    PMARK(PH_NHESS);
     // dense Cholesky (right-looking over the column-major lower-triangle table)
     int colstart = 0;
     for (int k = 0; k < nv; k++) {
@@ -1371,6 +1547,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
       }
       SYNC();
     }
+    PMARK(PH_NCHOL);
     // dir = -H^-1 g  (column-oriented substitutions)
     for (int i = LANE; i < nv; i += WAVE) dir[i] = -g[i];
     SYNC();
@@ -1388,6 +1565,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
       for (int i = LANE; i < k; i += WAVE) dir[i] -= H[k * nv + i] * xk;
       SYNC();
     }
+    PMARK(PH_NSOLVE);
     // exact line search along dir (segment walking over the breakpoints of the inequality rows)
     // Jd per contact (frame components) and per generic row
     for (int c = LANE; c < ncon; c += WAVE) {
@@ -1484,6 +1662,7 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
     SYNC();
     T newcost = quad(a) + rows_eval(M, w, a, ncon, nrow);
     SYNC();
+    PMARK(PH_NLS);
     T improvement = scale * (cost - newcost);
     cost = newcost;
     if (improvement < tol) {
@@ -1505,13 +1684,14 @@ __device__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ct
     rr[RR_F] = (ri[2] == 0 || rr[RR_JAR] < T(0)) ? -rr[RR_D] * rr[RR_JAR] : T(0);
   }
   SYNC();
+  PMARK(PH_NFINAL);
 }
 
 // ------------------------------------------------------------------------------------------------
 // step2: actuation, smooth acceleration, constraint solve, implicitfast integration
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__device__ void smooth_acc(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
+__device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
   const Dims& dm = M.dm;
   const int K = dm.K, nv = dm.nv;
   T* fa = w.fa();
@@ -1549,7 +1729,7 @@ __device__ void smooth_acc(const Model<T>& M, const Ws<T>& w, int arena, bool ac
   SYNC();
   // qacc_smooth = M^-1 qfrc_smooth
   int a0 = 1 + 6 * K;
-  for (int i = LANE; i < a0; i += WAVE) w.as()[i] = w.fs()[i] / Mdiag(M, arena, i);
+  for (int i = LANE; i < a0; i += WAVE) w.as()[i] = w.fs()[i] / Mdiag(M, w, i);
   if (LANE < dm.A) {
     T* L = w.Larm() + 81 * LANE;
     for (int k = 0; k < 81; k++) L[k] = w.Marm()[81 * LANE + k];
@@ -1563,7 +1743,7 @@ __device__ void smooth_acc(const Model<T>& M, const Ws<T>& w, int arena, bool ac
 }
 
 template <typename T>
-__device__ void implicit_integrate(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
+__device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
   const Dims& dm = M.dm;
   const int K = dm.K, nv = dm.nv;
   const T dt = M.dt;
@@ -1576,7 +1756,7 @@ __device__ void implicit_integrate(const Model<T>& M, const Ws<T>& w, int arena,
     T mb = M.belt_mass + dt * M.belt_damp + (actuation ? dt * M.belt_kv : T(0));
     acc[0] = (w.fs()[0] + w.fc()[0]) / mb;
   }
-  for (int i = 1 + LANE; i < a0; i += WAVE) acc[i] = (w.fs()[i] + w.fc()[i]) / Mdiag(M, arena, i);
+  for (int i = 1 + LANE; i < a0; i += WAVE) acc[i] = (w.fs()[i] + w.fc()[i]) / Mdiag(M, w, i);
   if (LANE < dm.A) {
     T* L = w.LBarm() + 81 * LANE;
     for (int k = 0; k < 81; k++) L[k] = w.Marm()[81 * LANE + k];
@@ -1642,6 +1822,7 @@ __device__ void implicit_integrate(const Model<T>& M, const Ws<T>& w, int arena,
   int qa0 = 1 + 7 * K;
   for (int i = LANE; i < 9 * dm.A; i += WAVE) q[qa0 + i] += dt * v[a0 + i];
   SYNC();
+  PMARK(PH_INT);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1666,7 +1847,7 @@ __device__ __forceinline__ double pcg_double(uint64_t* st) {
 }
 
 template <typename T>
-__device__ void hide_cube(const Dims& dm, T* q, T* v, int32_t* ti, int obj) {
+__device__ __forceinline__ void hide_cube(const Dims& dm, T* q, T* v, int32_t* ti, int obj) {
   ti[dm.K + ti[2 * dm.K + I_NOUT]] = obj;
   ti[2 * dm.K + I_NOUT]++;
   T* qq = q + 1 + 7 * obj;
@@ -1688,7 +1869,7 @@ __device__ __forceinline__ void pop_at(int32_t* list, int32_t* n, int idx) {
 
 // TaskManager.reset (task_utils.py:146-156) + BaseEnv.reset_sim bits (base_env.py:184-190)
 template <typename T>
-__device__ void task_reset(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, double* ctrl) {
+__device__ __forceinline__ void task_reset(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, double* ctrl) {
   const Dims& dm = M.dm;
   const int K = dm.K;
   for (int k = 0; k < K; k++) {
@@ -1716,7 +1897,7 @@ __device__ void task_reset(const Model<T>& M, T* q, T* v, int32_t* ti, double* t
 }
 
 template <typename T>
-__device__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr) {
+__device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr) {
   const Dims& dm = M.dm;
   const int K = dm.K;
   int32_t* ins = ti;
@@ -1782,8 +1963,71 @@ __device__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td,
 
 // observation row (environments.py:55-82 over base_env.py:149-175): arms (q[8], qd[8], ctrl[8]) then
 // in-scene cubes sorted by x (stable), zero padded: poses K x 7, velocities K x 6
+// lane 0: TaskManager.step, BaseEnv.step_sim bookkeeping (base_env.py:266-270), progress / score reward
+// (environments.py:129-149, 342-383), Monitor episode return; results in w.scal()
 template <typename T>
-__device__ void write_obs(const Model<T>& M, const Ws<T>& w, const int32_t* ti, float* obs) {
+__device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T>& w, int32_t* ti, double* td, uint64_t* rng,
+                                       int64_t* ctr, const float* act) {
+  const Dims& dm = M.dm;
+  const int A = dm.A, K = dm.K;
+  double* sc = w.scal();
+  int fail = task_step(M, w.q(), w.v(), ti, td, rng, ctr);
+  double dt_env = 0.001 * dm.frame_skip;
+  td[2] += dt_env;
+  td[1] += M.accel * dt_env;
+  td[0] *= M.spawn_inc;
+  int32_t* ts = ti + 2 * K;
+  int sd = (ts[I_S0] + ts[I_S1]) - (ts[I_LS0] + ts[I_LS1]);
+  double rew;
+  if (M.env_class == FM_ENV_FACTORY_SCORE) {
+    rew = sd;
+  } else {
+    double gc = 0, bc = 0;
+    double* lg = td + 3;
+    double* lb = td + 3 + A;
+    for (int i = 0; i < A; i++) {
+      if (ts[I_NIN] == 0) continue;
+      const T* gp = w.site() + 3 * i;
+      double best = 0;
+      int bi = -1;
+      for (int c = 0; c < ts[I_NIN]; c++) {
+        const T* qq = w.q() + 1 + 7 * ti[c];
+        double dx = (double)qq[0] - (double)gp[0], dy = (double)qq[1] - (double)gp[1],
+               dz = (double)qq[2] - (double)gp[2];
+        double dd = sqrt(dx * dx + dy * dy + dz * dz);
+        if (bi < 0 || dd < best) {
+          best = dd;
+          bi = c;
+        }
+      }
+      gc += lg[i] - best;
+      lg[i] = best;
+      // closest cube to this arm's bucket
+      const T* qq = w.q() + 1 + 7 * ti[bi];
+      double bx = (i % 2) == 0 ? M.bucket_x0 : M.bucket_x1;
+      double dx = (double)qq[0] - bx, dy = (double)qq[1] - M.bucket_y, dz = (double)qq[2] - M.bucket_z;
+      double db = sqrt(dx * dx + dy * dy + dz * dz);
+      bc += lb[i] - db;
+      lb[i] = db;
+    }
+    float ss = 0.0f;
+    for (int i = 0; i < 8 * A; i++)
+      if (i % 8 != 7) ss += act[i] * act[i];
+    float an = expf(-sqrtf(ss));
+    double prog = M.base_reward + M.w_grip * gc + M.w_bucket * bc + M.w_action * (double)an;
+    rew = sd > 0 ? (double)sd : prog;
+  }
+  ts[I_LS0] = ts[I_S0];
+  ts[I_LS1] = ts[I_S1];
+  sc[0] = rew;
+  sc[1] = (fail || sc[3] != 0.0) ? 1.0 : 0.0;
+  sc[2] = fail ? 1.0 : 0.0;
+  td[3 + 2 * A] += rew;  // Monitor episode return
+  ts[I_EPLEN]++;
+}
+
+template <typename T>
+__device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T>& w, const int32_t* ti, float* obs) {
   const Dims& dm = M.dm;
   const int A = dm.A, K = dm.K;
   const T* q = w.q();
@@ -1830,7 +2074,7 @@ __device__ void write_obs(const Model<T>& M, const Ws<T>& w, const int32_t* ti, 
 // kernels
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__device__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena, bool stage_copy) {
+__device__ __forceinline__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena, bool stage_copy) {
   const Dims& dm = M.dm;
   const T* ph = S.phys + (size_t)arena * dm.phys_stride;
   const T* src_q = ph + (stage_copy ? dm.nq + dm.nv : 0);
@@ -1839,21 +2083,38 @@ __device__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T>& w,
   for (int i = LANE; i < dm.nv; i += WAVE) w.v()[i] = src_v[i];
 }
 
+// per-launch LDS setup: geom / collision-body tables, static geom centres, body bounds, cube sizes
 template <typename T>
-__device__ void init_static_geoms(const Model<T>& M, const Ws<T>& w) {
-  for (int g = LANE; g < M.dm.ngc; g += WAVE) {
-    const int* gi = M.geom_i + 4 * g;
-    if (gi[2] != 0) continue;
+__device__ __forceinline__ void init_arena(const Model<T>& M, const Ws<T>& w, int arena) {
+  const Dims& dm = M.dm;
+  for (int g = LANE; g < dm.ngc; g += WAVE) {
+    const int gi = M.ginfo[g];
+    w.ginfo()[g] = gi;
     const T* gg = M.geom + 16 * g;
-    for (int c = 0; c < 3; c++) w.gx()[3 * g + c] = gg[c];
-    if (gi[3] >= 0)
-      for (int c = 0; c < 9; c++) w.gR()[9 * gi[3] + c] = gg[3 + c];
+    T* o = w.gx() + 4 * g;
+    const int kb = (gi >> 8) & 255;
+    if (kb == 0) {
+      o[0] = gg[0];
+      o[1] = gg[1];
+      o[2] = gg[2];
+    }
+    o[3] = gg[15];
+    w.cbg()[g] = M.cbg[g];
   }
+  for (int b = LANE; b < dm.ncb; b += WAVE) {
+    for (int k = 0; k < 4; k++) w.cbi()[4 * b + k] = M.cbi[4 * b + k];
+    for (int k = 0; k < 8; k++) w.cbw()[8 * b + k] = M.cbs[8 * b + k];
+    if (M.cbi[4 * b] == 1) {  // belt AABB: x, z fixed
+      w.cbw()[8 * b] = T(0);
+      w.cbw()[8 * b + 2] = T(1.05);
+    }
+  }
+  for (int i = LANE; i < 4 * dm.K; i += WAVE) w.cube()[i] = M.cube[(size_t)arena * dm.K * 4 + i];
 }
 
 // physics.reset() + TaskManager.reset() + after_reset forward (actuation disabled) -> warmstart
 template <typename T>
-__device__ void arena_reset(const Model<T>& M, const Ws<T>& w, int arena, int32_t* ti, double* td, int64_t* ctr) {
+__device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T>& w, int arena, int32_t* ti, double* td, int64_t* ctr) {
   const Dims& dm = M.dm;
   T* q = w.q();
   T* v = w.v();
@@ -1876,7 +2137,7 @@ __device__ void arena_reset(const Model<T>& M, const Ws<T>& w, int arena, int32_
 }
 
 template <typename T>
-__device__ void store_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena) {
+__device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena) {
   const Dims& dm = M.dm;
   T* ph = S.phys + (size_t)arena * dm.phys_stride;
   for (int i = LANE; i < dm.nq; i += WAVE) ph[i] = w.q()[i];
@@ -1896,7 +2157,7 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
   double* td = S.dbl + (size_t)arena * dm.dbl_stride + dm.nu;
   int64_t* ctr = S.counters + 4 * (size_t)arena;
-  init_static_geoms(M, w);
+  init_arena(M, w, arena);
   SYNC();
   arena_reset(M, w, arena, ti, td, ctr);
   // stage state = reset state
@@ -1919,6 +2180,7 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
   const Dims& dm = M.dm;
   const int A = dm.A, K = dm.K, nu = dm.nu;
   Ws<T> w{smem, &L};
+  if (M.prof && LANE < 16) w.prof()[LANE] = LANE == PH_LAST ? wall_clock64() : 0ull;
   int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
   double* td = S.dbl + (size_t)arena * dm.dbl_stride + nu;  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
   uint64_t* rng = S.rng + 4 * (size_t)arena;
@@ -1944,26 +2206,37 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
     double lo = (double)M.ctrlrange[2 * u], hi = (double)M.ctrlrange[2 * u + 1];
     uctl[u] = c < lo ? lo : (c > hi ? hi : c);
   }
-  init_static_geoms(M, w);
+  init_arena(M, w, arena);
   // warmstart
   const T* ph = S.phys + (size_t)arena * dm.phys_stride;
   for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
   SYNC();
-  // ---- stage at the state of the last mj_step1 (pre-teleport), then the current state
+  // stage (mj_step1) at the state of the last mj_step1 (pre-teleport), then integrate the current state
   load_state(M, S, w, arena, true);
   SYNC();
-  stage(M, w, arena, ctr);
-  load_state(M, S, w, arena, false);
-  SYNC();
   const double lp = 0.001 / (0.001 + M.pt_time);
-  bool force_term = false;
-  for (int t = 0; t < dm.frame_skip; t++) {
-    for (int u = LANE; u < nu; u += WAVE) {
-      double ct = ctrl[u] + (uctl[u] - ctrl[u]) * lp;
-      ctrl[u] = u == 0 ? -speed : ct;
+  T* phw = S.phys + (size_t)arena * dm.phys_stride;
+  double* sc = w.scal();  // [0] reward, [1] terminated, [2] out_of_reach, [3] force_terminate
+  bool reset_pass = false;
+  // Every physics phase has exactly one call site (the kernel is one loop), which keeps the code that a
+  // substep walks through small enough for the instruction cache:
+  //   t = 0..frame_skip-1:  mj_step1 (stage) ; ctrl low-pass ; mj_step2 (smooth acc, solve, integrate)
+  //   then the task layer; on termination one more pass = reset_sim's forward (stage, smooth, solve).
+  for (int t = 0;; t++) {
+    stage(M, w, arena, ctr);
+    if (t == 0 && !reset_pass) {
+      load_state(M, S, w, arena, false);
+      SYNC();
     }
-    SYNC();
-    smooth_acc(M, w, arena, true);
+    if (!reset_pass) {
+      for (int u = LANE; u < nu; u += WAVE) {
+        double ct = ctrl[u] + (uctl[u] - ctrl[u]) * lp;
+        ctrl[u] = u == 0 ? -speed : ct;
+      }
+      SYNC();
+    }
+    smooth_acc(M, w, arena, !reset_pass);
+    PMARK(PH_SMOOTH);
     if (w.misc()[MISC_NCON] + w.misc()[MISC_NROW] > 0) {
       newton(M, w, arena, ctr);
     } else {
@@ -1973,9 +2246,11 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
       }
       SYNC();
     }
+    if (reset_pass) break;
     implicit_integrate(M, w, arena, true);
-    if (t == dm.frame_skip - 1) {
-      // contact-force termination on the contacts + forces of the final solve
+    if (t < dm.frame_skip - 1) continue;
+    // ---- end of the env-step: contact-force termination on the contacts + forces of the final solve
+    {
       int ncon = w.misc()[MISC_NCON];
       bool hit = false;
       for (int c = LANE; c < ncon; c += WAVE) {
@@ -1990,121 +2265,67 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
         mx = fabs(f2) > mx ? fabs(f2) : mx;
         if ((double)mx > M.force_thr) hit = true;
       }
-      force_term = __ballot(hit) != 0ull;
-    } else {
-      stage(M, w, arena, ctr);
+      if (LANE == 0) sc[3] = __ballot(hit) != 0ull ? 1.0 : 0.0;
     }
-  }
-  // gripper sites at the final state (the last mj_step1's site_xpos)
-  if (LANE < A) arm_chain(M, w, LANE, false);
-  SYNC();
-  // stage state for the next env-step = state before the TaskManager's teleports
-  T* phw = S.phys + (size_t)arena * dm.phys_stride;
-  for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
-  for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
-  double* sc = w.scal();  // [0] reward, [1] terminated, [2] out_of_reach
-  if (LANE == 0) {
-    int fail = task_step(M, w.q(), w.v(), ti, td, rng, ctr);
-    // BaseEnv.step_sim bookkeeping (base_env.py:266-270)
-    double dt_env = 0.001 * dm.frame_skip;
-    td[2] += dt_env;
-    td[1] += M.accel * dt_env;
-    td[0] *= M.spawn_inc;
-    int32_t* ts = ti + 2 * K;
-    int sd = (ts[I_S0] + ts[I_S1]) - (ts[I_LS0] + ts[I_LS1]);
-    double rew;
-    if (M.env_class == FM_ENV_FACTORY_SCORE) {
-      rew = sd;
-    } else {
-      double gc = 0, bc = 0;
-      int closest[16];
-      double* lg = td + 3;
-      double* lb = td + 3 + A;
-      for (int i = 0; i < A; i++) {
-        closest[i] = -1;
-        if (ts[I_NIN] == 0) continue;
-        const T* gp = w.site() + 3 * i;
-        double best = 0;
-        int bi = -1;
-        for (int c = 0; c < ts[I_NIN]; c++) {
-          const T* qq = w.q() + 1 + 7 * ti[c];
-          double dx = (double)qq[0] - (double)gp[0], dy = (double)qq[1] - (double)gp[1],
-                 dz = (double)qq[2] - (double)gp[2];
-          double dd = sqrt(dx * dx + dy * dy + dz * dz);
-          if (bi < 0 || dd < best) {
-            best = dd;
-            bi = c;
-          }
-        }
-        closest[i] = ti[bi];
-        gc += lg[i] - best;
-        lg[i] = best;
-      }
-      for (int i = 0; i < A; i++) {
-        if (closest[i] < 0) continue;
-        const T* qq = w.q() + 1 + 7 * closest[i];
-        double bx = (i % 2) == 0 ? M.bucket_x0 : M.bucket_x1;
-        double dx = (double)qq[0] - bx, dy = (double)qq[1] - M.bucket_y, dz = (double)qq[2] - M.bucket_z;
-        double dd = sqrt(dx * dx + dy * dy + dz * dz);
-        bc += lb[i] - dd;
-        lb[i] = dd;
-      }
-      float ss = 0.0f;
-      for (int i = 0; i < 8 * A; i++)
-        if (i % 8 != 7) ss += act[i] * act[i];
-      float an = expf(-sqrtf(ss));
-      double prog = M.base_reward + M.w_grip * gc + M.w_bucket * bc + M.w_action * (double)an;
-      rew = sd > 0 ? (double)sd : prog;
-    }
-    ts[I_LS0] = ts[I_S0];
-    ts[I_LS1] = ts[I_S1];
-    sc[0] = rew;
-    sc[1] = (fail || force_term) ? 1.0 : 0.0;
-    sc[2] = fail ? 1.0 : 0.0;
-    td[3 + 2 * A] += rew;  // Monitor episode return
-    ts[I_EPLEN]++;
-  }
-  SYNC();
-  const int term = sc[1] != 0.0;
-  const int s_fail = sc[2] != 0.0;
-  const double s_rew = sc[0];
-  if (LANE == 0) {
-    int32_t* ts = ti + 2 * K;
-    if (io.reward) io.reward[arena] = (float)s_rew;
-    if (io.terminated) io.terminated[arena] = (uint8_t)term;
-    if (io.truncated) io.truncated[arena] = 0;
-    if (io.scores) {
-      io.scores[2 * arena] = ts[I_S0];
-      io.scores[2 * arena + 1] = ts[I_S1];
-    }
-    if (io.num_obj) io.num_obj[arena] = ts[I_NIN];
-    if (io.play_time) io.play_time[arena] = td[2];
-    if (io.conveyor_speed) io.conveyor_speed[arena] = td[1];
-    if (io.out_of_reach) io.out_of_reach[arena] = (uint8_t)s_fail;
-    if (io.force_terminate) io.force_terminate[arena] = (uint8_t)force_term;
-    if (term) {
-      if (io.ep_return) io.ep_return[arena] = td[3 + 2 * A];
-      if (io.ep_len) io.ep_len[arena] = ts[I_EPLEN];
-      if (io.terminal_scores) {
-        io.terminal_scores[2 * arena] = ts[I_S0];
-        io.terminal_scores[2 * arena + 1] = ts[I_S1];
-      }
-    }
-  }
-  if (term) {
-    if (io.terminal_obs) write_obs(M, w, ti, io.terminal_obs + (size_t)arena * dm.obs_dim);
+    // gripper sites at the final state (the last mj_step1's site_xpos)
+    if (LANE < A) arm_chain(M, w, LANE, false);
     SYNC();
-    arena_reset(M, w, arena, ti, td, ctr);
+    // stage state for the next env-step = state before the TaskManager's teleports
     for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
     for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
+    if (LANE == 0) task_tail(M, w, ti, td, rng, ctr, act);
+    SYNC();
+    const int term = sc[1] != 0.0;
     if (LANE == 0) {
+      const int s_fail = sc[2] != 0.0;
+      const bool force_term = sc[3] != 0.0;
+      int32_t* ts = ti + 2 * K;
+      if (io.reward) io.reward[arena] = (float)sc[0];
+      if (io.terminated) io.terminated[arena] = (uint8_t)term;
+      if (io.truncated) io.truncated[arena] = 0;
+      if (io.scores) {
+        io.scores[2 * arena] = ts[I_S0];
+        io.scores[2 * arena + 1] = ts[I_S1];
+      }
+      if (io.num_obj) io.num_obj[arena] = ts[I_NIN];
+      if (io.play_time) io.play_time[arena] = td[2];
+      if (io.conveyor_speed) io.conveyor_speed[arena] = td[1];
+      if (io.out_of_reach) io.out_of_reach[arena] = (uint8_t)s_fail;
+      if (io.force_terminate) io.force_terminate[arena] = (uint8_t)force_term;
+      if (term) {
+        if (io.ep_return) io.ep_return[arena] = td[3 + 2 * A];
+        if (io.ep_len) io.ep_len[arena] = ts[I_EPLEN];
+        if (io.terminal_scores) {
+          io.terminal_scores[2 * arena] = ts[I_S0];
+          io.terminal_scores[2 * arena + 1] = ts[I_S1];
+        }
+      }
+    }
+    if (!term) break;
+    // ---- auto-reset (reset_sim, base_env.py:177-198): terminal obs, zero state, TaskManager.reset,
+    // then one more pass of this loop = the forward at the reset state that leaves qacc_warmstart
+    if (io.terminal_obs) write_obs(M, w, ti, io.terminal_obs + (size_t)arena * dm.obs_dim);
+    SYNC();
+    for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = T(0);
+    for (int i = LANE; i < dm.nv; i += WAVE) {
+      w.v()[i] = T(0);
+      w.a()[i] = T(0);
+    }
+    SYNC();
+    if (LANE == 0) {
+      task_reset(M, w.q(), w.v(), ti, td, w.ctrl());
       td[3 + 2 * A] = 0.0;
       ti[2 * K + I_EPLEN] = 0;
     }
     SYNC();
+    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
+    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
+    reset_pass = true;
   }
   store_state(M, S, w, arena);
   if (io.obs) write_obs(M, w, ti, io.obs + (size_t)arena * dm.obs_dim);
+  PMARK(PH_TAIL);
+  if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);
 }
 
 
@@ -2123,7 +2344,7 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < dm.nu; u += WAVE) w.ctrl()[u] = dsrc[u];
   for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
-  init_static_geoms(M, w);
+  init_arena(M, w, arena);
   SYNC();
   load_state(M, S, w, arena, true);
   SYNC();
@@ -2229,6 +2450,11 @@ struct fm_handle {
   void* ctrlrange = nullptr;
   void* geom = nullptr;
   int* geom_i = nullptr;
+  int* ginfo = nullptr;
+  int* cbi = nullptr;
+  void* cbs = nullptr;
+  uint16_t* cbg = nullptr;
+  uint32_t* cbp = nullptr;
   uint32_t* pair = nullptr;
   void* param = nullptr;
   void* cube = nullptr;
@@ -2240,6 +2466,8 @@ struct fm_handle {
   int32_t* ints = nullptr;
   uint64_t* rng = nullptr;
   int64_t* counters = nullptr;
+  unsigned long long* prof = nullptr;
+  bool prof_on = false;
 };
 
 template <typename T>
@@ -2300,19 +2528,29 @@ static Lay lds_layout(const Dims& d, int tsize) {
   L.Marm = take(tsize * 81 * A);
   L.Larm = take(tsize * 81 * A);
   L.LBarm = take(tsize * 81 * A);
-  L.gx = take(tsize * 3 * d.ngc);
-  L.gR = take(tsize * 9 * d.nbox);
+  L.gx = take(tsize * 4 * d.ngc);
+  L.ginfo = take(4 * d.ngc);
+  L.cbi = take(4 * 4 * d.ncb);
+  L.cbw = take(tsize * 8 * d.ncb);
+  L.cbg = take(2 * d.ngc);
+  L.sp = take(4 * WAVE);
+  L.spoff = take(4 * WAVE);
+  L.gsurv = take(4 * 2 * WAVE);
+  L.stage = take(tsize * 8 * d.maxcon);
+  L.skey = take(4 * d.maxcon);
+  L.spw = take(4 * d.maxcon);
+  L.cube = take(tsize * 4 * d.K);
   L.H = take(tsize * nv * nv);
   L.c_i = take(4 * 4 * d.maxcon);
   L.c_r = take(tsize * CR_N * d.maxcon);
   L.r_i = take(4 * 4 * d.maxrow);
   L.r_r = take(tsize * RR_N * d.maxrow);
-  L.surv = take(2 * MAXSURV);
   L.tmask = take(8 * d.ntree);
   L.misc = take(4 * 16);
   L.sort = take(4 * K);
   L.uctl = take(8 * d.nu);
   L.scal = take(8 * 4);
+  L.prof = take(8 * 16);
   L.total = off;
   return L;
 }
@@ -2352,10 +2590,18 @@ static Model<T> make_model(const fm_handle* h) {
   M.geom = (const T*)h->geom;
   M.geom_i = h->geom_i;
   M.pair = h->pair;
+  M.ginfo = h->ginfo;
+  M.cbi = h->cbi;
+  M.cbs = (const T*)h->cbs;
+  M.cbg = h->cbg;
+  M.cbp = h->cbp;
+  for (int a = 0; a < 5; a++)
+    for (int b = 0; b < 5; b++) M.ptab[5 * a + b] = h->sc.ptab[a][b];
   M.param = (const T*)h->param;
   M.cube = (const T*)h->cube;
   M.meaninertia = (const T*)h->meaninertia;
   M.tri = h->tri;
+  M.prof = h->prof_on ? h->prof : nullptr;
   return M;
 }
 
@@ -2427,6 +2673,33 @@ static int create_typed(fm_handle* h) {
   if ((r = upload<T>(h, &h->geom, geom))) return r;
   if ((r = upload_raw<int>(h, &h->geom_i, geom_i))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->pair, s.pairs))) return r;
+  {
+    std::vector<int> gin(ngc), cbi(4 * s.cbodies.size());
+    std::vector<double> cbs(8 * s.cbodies.size(), 0.0);
+    for (int g = 0; g < ngc; g++) {
+      const GeomRec& G = s.geoms[g];
+      int tc = G.type == GT_PLANE ? GC_PLANE : (G.type == GT_SPHERE ? GC_SPHERE : GC_BOX);
+      int arm = G.mjid >= 13 + s.K ? 1 : 0;
+      gin[g] = tc | (arm << GI_ARM) | (G.pclass << GI_PC) | (G.kbody << 8);
+    }
+    for (size_t b = 0; b < s.cbodies.size(); b++) {
+      const CBody& c = s.cbodies[b];
+      cbi[4 * b] = c.kbody;
+      cbi[4 * b + 1] = c.flags;
+      cbi[4 * b + 2] = c.g0;
+      cbi[4 * b + 3] = c.ng;
+      for (int k = 0; k < 3; k++) {
+        cbs[8 * b + k] = c.c[k];
+        cbs[8 * b + 4 + k] = c.e[k];
+      }
+      cbs[8 * b + 3] = c.r;
+    }
+    if ((r = upload_raw<int>(h, &h->ginfo, gin))) return r;
+    if ((r = upload_raw<int>(h, &h->cbi, cbi))) return r;
+    if ((r = upload<T>(h, &h->cbs, cbs))) return r;
+    if ((r = upload_raw<uint16_t>(h, &h->cbg, s.cb_geoms))) return r;
+    if ((r = upload_raw<uint32_t>(h, &h->cbp, s.cb_pairs))) return r;
+  }
   if ((r = upload<T>(h, &h->param, param))) return r;
   if ((r = upload<T>(h, &h->cube, s.cube))) return r;
   if ((r = upload<T>(h, &h->meaninertia, s.meaninertia))) return r;
@@ -2572,6 +2845,8 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
   d.npair = (int)s.pairs.size();
   d.nparam = (int)s.params.size();
   d.ntree = 1 + s.K + s.A;
+  d.ncb = (int)s.cbodies.size();
+  d.ncbp = (int)s.cb_pairs.size();
   d.obs_dim = s.obs_dim;
   d.act_dim = s.act_dim;
   d.frame_skip = (int)((1.0 / cfg->control_frequency) / 0.001);
@@ -2722,6 +2997,31 @@ int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int c
   HIPCHK(hipMemcpy(host_out, dbuf, need * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(dbuf));
   return need;
+}
+
+int fm_profile(fm_handle* h, int mode, uint64_t* host_out) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  if (!h->prof) {
+    HIPCHK(hipMalloc((void**)&h->prof, 16 * sizeof(unsigned long long)));
+    h->allocs.push_back(h->prof);
+    HIPCHK(hipMemset(h->prof, 0, 16 * sizeof(unsigned long long)));
+  }
+  if (host_out) {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(host_out, h->prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    int khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
+    host_out[15] = (uint64_t)khz;
+  }
+  if (mode == 1) {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemset(h->prof, 0, 16 * sizeof(unsigned long long)));
+    h->prof_on = true;
+  } else if (mode == 0) {
+    h->prof_on = false;
+  }
+  return FM_OK;
 }
 
 int fm_get_counters(fm_handle* h, int64_t* host_out) {

@@ -524,6 +524,131 @@ bool build_scene(int A, int K, int N, const uint64_t* seeds, SceneHost& s, std::
     err = "scene too large for the pair encoding";
     return false;
   }
+  for (int a = 0; a < 5; a++)
+    for (int b = 0; b < 5; b++) {
+      ParamRec p = mix_params(a, b);
+      auto key = std::make_tuple((long long)std::llround(p.mu * 1e9), (long long)std::llround(p.solref[0] * 1e12),
+                                 (long long)std::llround(p.solimp[0] * 1e9 + p.solimp[1] * 1e3));
+      auto it = pidx.find(key);
+      if (it == pidx.end()) {
+        s.ptab[a][b] = (int)s.params.size();
+        pidx[key] = s.ptab[a][b];
+        s.params.push_back(p);
+      } else {
+        s.ptab[a][b] = it->second;
+      }
+    }
+
+  // ---- collision bodies: each moving kernel body; static geoms grouped (floor, table, bucket b, arm base i)
+  {
+    std::vector<int> cb_of(ng, -1);
+    std::vector<std::vector<int>> members;
+    std::map<long long, int> idx;
+    auto group = [&](long long key, int kb, int flags) {
+      auto it = idx.find(key);
+      if (it != idx.end()) return it->second;
+      CBody c{};
+      c.kbody = kb;
+      c.flags = flags;
+      s.cbodies.push_back(c);
+      members.emplace_back();
+      idx[key] = (int)s.cbodies.size() - 1;
+      return (int)s.cbodies.size() - 1;
+    };
+    for (int g = 0; g < ng; g++) {
+      const GeomRec& G = s.geoms[g];
+      int cb;
+      if (G.kbody == 0) {
+        if (G.type == GT_PLANE)
+          cb = group(-1, 0, CB_STATIC | CB_PLANE);
+        else if (G.mjid == 1)
+          cb = group(-2, 0, CB_STATIC);
+        else if (G.mjid >= 3 + K && G.mjid < 13 + K)
+          cb = group(-3 - (G.mjid - 3 - K) / 5, 0, CB_STATIC);
+        else
+          cb = group(-10 - (G.mjid - 13 - K) / 70, 0, CB_STATIC);
+      } else {
+        cb = group(G.kbody, G.kbody, G.kbody == 1 ? CB_BELT : 0);
+      }
+      cb_of[g] = cb;
+      members[cb].push_back(g);
+    }
+    if (s.cbodies.size() > 255) {
+      err = "too many collision bodies";
+      return false;
+    }
+    s.cb_geoms.clear();
+    for (size_t b = 0; b < s.cbodies.size(); b++) {
+      CBody& c = s.cbodies[b];
+      c.g0 = (int)s.cb_geoms.size();
+      c.ng = (int)members[b].size();
+      for (int g : members[b]) s.cb_geoms.push_back((uint16_t)g);
+      double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+      c.r = 0;
+      for (int g : members[b]) {
+        const GeomRec& G = s.geoms[g];
+        if (c.flags & CB_STATIC) {
+          if (G.type == GT_PLANE) continue;
+          for (int i = 0; i < 8; i++) {
+            double cl[3] = {0, 0, 0}, cw[3];
+            if (G.type == GT_BOX) {
+              cl[0] = (i & 1) ? G.size[0] : -G.size[0];
+              cl[1] = (i & 2) ? G.size[1] : -G.size[1];
+              cl[2] = (i & 4) ? G.size[2] : -G.size[2];
+            } else {
+              cl[0] = (i & 1) ? G.size[0] : -G.size[0];
+              cl[1] = (i & 2) ? G.size[0] : -G.size[0];
+              cl[2] = (i & 4) ? G.size[0] : -G.size[0];
+            }
+            matvec3(G.R, cl, cw);
+            for (int k = 0; k < 3; k++) {
+              lo[k] = std::min(lo[k], G.pos[k] + cw[k]);
+              hi[k] = std::max(hi[k], G.pos[k] + cw[k]);
+            }
+          }
+        } else if (c.flags & CB_BELT) {
+          for (int k = 0; k < 3; k++) c.e[k] = G.size[k];
+        } else if (G.kbody >= 2 && G.kbody < 2 + K) {
+          c.r = std::sqrt(3.0) * 0.05;  // largest cube (h <= 0.05), about the cube centre
+        } else {
+          double d = std::sqrt(G.pos[0] * G.pos[0] + G.pos[1] * G.pos[1] + G.pos[2] * G.pos[2]);
+          c.r = std::max(c.r, d + G.rbound);
+        }
+      }
+      if ((c.flags & CB_STATIC) && !(c.flags & CB_PLANE))
+        for (int k = 0; k < 3; k++) {
+          c.c[k] = 0.5 * (lo[k] + hi[k]);
+          c.e[k] = 0.5 * (hi[k] - lo[k]);
+        }
+    }
+    // allowed body pairs: MuJoCo's filters are per body, so every geom pair of a body pair agrees
+    auto allowed = [&](int a, int b) {
+      const GeomRec& ga = s.geoms[a];
+      const GeomRec& gbr = s.geoms[b];
+      if (ga.weld == gbr.weld) return false;
+      if (ga.weld != 0 && gbr.weld != 0 && (ga.weld == gbr.weldparent || gbr.weld == ga.weldparent)) return false;
+      std::pair<int, int> bp{std::min(ga.mjbody, gbr.mjbody), std::max(ga.mjbody, gbr.mjbody)};
+      return std::find(excl.begin(), excl.end(), bp) == excl.end();
+    };
+    s.cb_pairs.clear();
+    int ncb = (int)s.cbodies.size();
+    for (int x = 0; x < ncb; x++)
+      for (int y = x + 1; y < ncb; y++) {
+        if ((s.cbodies[x].flags & CB_STATIC) && (s.cbodies[y].flags & CB_STATIC)) continue;
+        int na = 0, nt = 0;
+        for (int g : members[x])
+          for (int h : members[y]) {
+            nt++;
+            na += allowed(g, h) ? 1 : 0;
+          }
+        if (na == 0) continue;
+        if (na != nt) {
+          err = "collision filter is not uniform over a body pair";
+          return false;
+        }
+        s.cb_pairs.push_back((uint32_t)x | ((uint32_t)y << 8));
+      }
+  }
 
   // ---- per-arena cubes (scene.py:121-131: draws size, rgba[4] per cube) and constants
   s.cube.assign((size_t)N * K * 4, 0.0);

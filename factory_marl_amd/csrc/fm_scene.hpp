@@ -36,6 +36,17 @@ struct GeomRec {
   double rbound;
 };
 
+// collision body: the unit of the broadphase (one moving kernel body, or a group of static geoms)
+enum { CB_STATIC = 1, CB_PLANE = 2, CB_BELT = 4 };
+struct CBody {
+  int kbody;      // kernel body code (0 for static groups)
+  int flags;      // CB_*
+  double c[3];    // static: world AABB centre
+  double e[3];    // static / belt: AABB half extents
+  double r;       // moving: bounding radius about the body origin (cubes: about the centre)
+  int g0, ng;     // range in cb_geoms
+};
+
 struct ParamRec {
   double mu, solref[2], solimp[5];
 };
@@ -58,6 +69,11 @@ struct SceneHost {
   std::vector<uint32_t> pairs;  // c1 | c2 << 12 | param << 24  (compact geom indices, type-ordered)
   int nbox = 0;
   std::vector<int> box_slot;    // per compact geom, -1 for non-box
+  // two-level broadphase: collision bodies, their geoms, the body pairs MuJoCo's filters allow
+  std::vector<CBody> cbodies;
+  std::vector<uint16_t> cb_geoms;
+  std::vector<uint32_t> cb_pairs;  // b1 | b2 << 8 (b1 < b2)
+  int ptab[5][5];                  // params index for (pclass g1, pclass g2)
   // per arena
   std::vector<double> cube;     // [N][K][4]: h, m, I, pad
   std::vector<double> meaninertia;  // [N]

@@ -127,6 +127,13 @@ int fm_set_state(fm_handle* h, const void* host_in);
  * anomalies (task_utils.py:103-113 would raise IndexError). */
 int fm_get_counters(fm_handle* h, int64_t* host_out);
 
+/* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [16] uint64).
+ * mode 1 = zero and enable, 0 = disable, -1 = leave as is; host_out (may be NULL) receives the
+ * totals: [0..13] clock ticks per phase (FK, geoms+M, collision, constraint rows, smooth acc,
+ * Newton setup / gradient / Hessian / Cholesky / solve / line search / final forces, integration,
+ * task+obs), [14] sum of ncon over stages, [15] the clock rate in kHz. */
+int fm_profile(fm_handle* h, int mode, uint64_t* host_out);
+
 /* Diagnostic (tests only): recompute one mj_step1 + acceleration stage of `arena` at its stored stage
  * state and dump internals as float64 into host_out (capacity `cap` doubles).  Returns the number of
  * doubles written (< 0 on error).  Layout in factory_marl_amd/csrc/fm_kernel.hip (debug_kernel). */

@@ -6,8 +6,9 @@
  *   parameter mixing by priority / solmix (mj_contactParam); contact frame via mju_makeFrame.
  * Narrowphase: mjc_PlaneSphere, mjc_PlaneBox and mjc_SphereSphere follow MuJoCo's published formulas.
  * Sphere-box and box-box are this project's own definitions: MuJoCo's mjc_BoxBox
- * is not available here, so box-box is SAT over 15 axes + reference-face clipping (<= 8 points),
- * edge-edge as a single point; the HIP kernel implements the same definition.
+ * is not available here, so box-box is SAT over 15 axes; a face contact yields the vertices of the
+ * incident-face / reference-face intersection (<= 8 points), edge-edge a single point; the HIP kernel
+ * implements the same definition.
  */
 #include <stdlib.h>
 
@@ -215,7 +216,12 @@ int or_box_box(const double* p1, const double* R1, const double* h1, const doubl
     set_con(out, -best_edge, pos, n);
     return 1;
   }
-  /* face contact */
+  /* face contact: the vertices of the intersection of the incident face with the reference face,
+   * enumerated as (1) incident vertices inside the reference rectangle, (2) reference corners inside
+   * the incident quad (projected along the reference normal), (3) proper crossings of incident edges
+   * with the rectangle's sides; each kept if it penetrates.  Boundary conventions make every polygon
+   * vertex appear once: (1) closed rectangle, (2) open quad, (3) u-sides closed / v-sides open.  Worked in reference-face coordinates
+   * (u along ar[t1], v along ar[t2], w along nref, origin at the face centre). */
   double sg = face_s >= 0 ? 1.0 : -1.0;
   double n[3];
   for (int k = 0; k < 3; k++) n[k] = face_u[k] * sg;
@@ -233,7 +239,9 @@ int or_box_box(const double* p1, const double* R1, const double* h1, const doubl
   double fc[3];
   for (int k = 0; k < 3; k++) fc[k] = pr[k] + nref[k] * hr[kr];
   int t1 = (kr + 1) % 3, t2 = (kr + 2) % 3;
-  /* incident face */
+  const double *ta = ar[t1], *tb = ar[t2];
+  double e1 = hr[t1], e2 = hr[t2];
+  /* incident face: the incident box axis most anti-parallel to nref */
   int mi = 0;
   double bestdot = -1;
   for (int k = 0; k < 3; k++) {
@@ -244,44 +252,75 @@ int or_box_box(const double* p1, const double* R1, const double* h1, const doubl
     }
   }
   double sgn = or_dot3(nref, ai[mi]) > 0 ? -1.0 : 1.0;
-  double ic[3];
-  for (int k = 0; k < 3; k++) ic[k] = pi[k] + sgn * hi[mi] * ai[mi][k];
   int u1 = (mi + 1) % 3, u2 = (mi + 2) % 3;
-  double poly[16][3], tmp[16][3];
+  double icr[3];
+  for (int k = 0; k < 3; k++) icr[k] = pi[k] + sgn * hi[mi] * ai[mi][k] - fc[k];
+  double cu = or_dot3(icr, ta), cv = or_dot3(icr, tb), cw = or_dot3(icr, nref);
+  double a1u = hi[u1] * or_dot3(ai[u1], ta), a1v = hi[u1] * or_dot3(ai[u1], tb), a1w = hi[u1] * or_dot3(ai[u1], nref);
+  double a2u = hi[u2] * or_dot3(ai[u2], ta), a2v = hi[u2] * or_dot3(ai[u2], tb), a2w = hi[u2] * or_dot3(ai[u2], nref);
   const double sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
-  for (int v = 0; v < 4; v++)
-    for (int k = 0; k < 3; k++) poly[v][k] = ic[k] + sx[v] * hi[u1] * ai[u1][k] + sy[v] * hi[u2] * ai[u2][k];
-  int np = 4;
-  for (int pl = 0; pl < 4 && np > 0; pl++) {
-    const double* t = ar[pl < 2 ? t1 : t2];
-    double e = hr[pl < 2 ? t1 : t2];
-    double sside = (pl & 1) ? -1.0 : 1.0;
-    int nn = 0;
-    for (int v = 0; v < np; v++) {
-      const double* P = poly[v];
-      const double* Q = poly[(v + 1) % np];
-      double rp[3] = {P[0] - fc[0], P[1] - fc[1], P[2] - fc[2]};
-      double rq[3] = {Q[0] - fc[0], Q[1] - fc[1], Q[2] - fc[2]};
-      double dp = e - sside * or_dot3(rp, t);
-      double dq = e - sside * or_dot3(rq, t);
-      if (dp >= 0) memcpy(tmp[nn++], P, 3 * sizeof(double));
-      if ((dp >= 0) != (dq >= 0)) {
+  double U[4], V[4], W[4];
+  for (int k = 0; k < 4; k++) {
+    U[k] = cu + sx[k] * a1u + sy[k] * a2u;
+    V[k] = cv + sx[k] * a1v + sy[k] * a2v;
+    W[k] = cw + sx[k] * a1w + sy[k] * a2w;
+  }
+  double cand[24][3];
+  int nc = 0;
+  /* (1) */
+  for (int k = 0; k < 4; k++)
+    if (fabs(U[k]) <= e1 && fabs(V[k]) <= e2) {
+      cand[nc][0] = U[k];
+      cand[nc][1] = V[k];
+      cand[nc][2] = W[k];
+      nc++;
+    }
+  /* (2) */
+  double det = a1u * a2v - a2u * a1v;
+  double ia = a1w * a2v - a2w * a1v, ib = a1u * a2w - a2u * a1w;
+  for (int k = 0; k < 4; k++) {
+    double cu_ = sx[k] * e1, cv_ = sy[k] * e2;
+    int in = det != 0;
+    for (int m = 0; m < 4; m++) {
+      int m1 = (m + 1) & 3;
+      double cr = (U[m1] - U[m]) * (cv_ - V[m]) - (V[m1] - V[m]) * (cu_ - U[m]);
+      in = in && (det >= 0 ? cr > 0 : cr < 0);
+    }
+    if (in) {
+      cand[nc][0] = cu_;
+      cand[nc][1] = cv_;
+      cand[nc][2] = cw + (ia * (cu_ - cu) + ib * (cv_ - cv)) / det;
+      nc++;
+    }
+  }
+  /* (3) */
+  for (int m = 0; m < 4; m++) {
+    int m1 = (m + 1) & 3;
+    for (int sd = 0; sd < 4; sd++) {
+      int onu = sd < 2;
+      double ss = (sd & 1) ? -1.0 : 1.0;
+      double e = onu ? e1 : e2;
+      double dp = e - ss * (onu ? U[m] : V[m]);
+      double dq = e - ss * (onu ? U[m1] : V[m1]);
+      if ((dp > 0 && dq < 0) || (dp < 0 && dq > 0)) {
         double f = dp / (dp - dq);
-        for (int k = 0; k < 3; k++) tmp[nn][k] = P[k] + (Q[k] - P[k]) * f;
-        nn++;
+        double xu = U[m] + (U[m1] - U[m]) * f, xv = V[m] + (V[m1] - V[m]) * f, xw = W[m] + (W[m1] - W[m]) * f;
+        if (onu ? fabs(xv) <= e2 : fabs(xu) < e1) {
+          cand[nc][0] = xu;
+          cand[nc][1] = xv;
+          cand[nc][2] = xw;
+          nc++;
+        }
       }
     }
-    np = nn;
-    memcpy(poly, tmp, nn * sizeof(poly[0]));
   }
   int cnt = 0;
-  for (int v = 0; v < np && cnt < 8; v++) {
-    double rv[3] = {fc[0] - poly[v][0], fc[1] - poly[v][1], fc[2] - poly[v][2]};
-    double depth = or_dot3(rv, nref);
-    if (depth < -margin) continue;
-    double pos[3];
-    for (int k = 0; k < 3; k++) pos[k] = poly[v][k] + nref[k] * depth / 2;
-    set_con(out + cnt, -depth, pos, n);
+  for (int c = 0; c < nc && cnt < 8; c++) {
+    double u = cand[c][0], v = cand[c][1], w = cand[c][2];
+    if (w > margin) continue;
+    double hw = 0.5 * w, pos[3];
+    for (int k = 0; k < 3; k++) pos[k] = fc[k] + u * ta[k] + v * tb[k] + hw * nref[k];
+    set_con(out + cnt, w, pos, n);
     cnt++;
   }
   return cnt;

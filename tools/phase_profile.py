@@ -1,0 +1,50 @@
+"""Phase profile of the env-step kernel (fm_profile): where the wall time of one env-step goes.
+
+Usage (GPU box): python tools/phase_profile.py [--arenas 4096] [--steps 10] [--precision fp32]
+Times are wall-clock ticks summed over arenas, so they are reported as a share of the total and as
+microseconds per arena-substep.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arenas", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--precision", default="fp32")
+    args = ap.parse_args()
+    import torch
+
+    from factory_marl_amd import FactoryVecEnv
+
+    env = FactoryVecEnv(args.arenas, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42),
+                        precision=args.precision)
+    env.reset()
+    g = torch.Generator(device=env.device)
+    g.manual_seed(0)
+    for _ in range(5):
+        env.step_tensors(torch.rand(args.arenas, env.act_dim, device=env.device, generator=g) * 2 - 1)
+    env.sync()
+    c0 = env.counters().sum(0)
+    env.profile(1)
+    for _ in range(args.steps):
+        env.step_tensors(torch.rand(args.arenas, env.act_dim, device=env.device, generator=g) * 2 - 1)
+    env.sync()
+    ph, ncon = env.profile(0)
+    c1 = env.counters().sum(0)
+    tot = sum(ph.values())
+    sub = args.arenas * args.steps * 100
+    rep = {k: {"share": round(v / tot, 4), "us_per_arena_substep": round(v / sub * 1e6, 3)} for k, v in ph.items()}
+    rep["_total_us_per_arena_substep"] = round(tot / sub * 1e6, 3)
+    rep["_mean_ncon"] = round(ncon / sub, 3)
+    rep["_newton_iters_per_substep"] = round(float(c1[1] - c0[1]) / sub, 3)
+    print(json.dumps(rep, indent=1))
+
+
+if __name__ == "__main__":
+    main()
