@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfactorysim.so")
+LIB_PATH = os.environ.get("FACTORYSIM_LIB", os.path.join(_HERE, "libfactorysim.so"))
 
 FM_ENV_FACTORY_SCORE = 0
 FM_ENV_ALLFULLRL_PROGRESS = 1
@@ -56,7 +56,7 @@ class FmInfo(C.Structure):
 
 EXPORTED = [
     "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
-    "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_reset", "fm_step", "fm_state_size",
+    "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
     "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile",
 ]
 
@@ -88,7 +88,7 @@ def load():
     L.fm_set_stream.restype = I
     L.fm_sync.argtypes = [P]
     L.fm_sync.restype = I
-    for n in ["fm_obs_dim", "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_state_size"]:
+    for n in ["fm_obs_dim", "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_state_size"]:
         getattr(L, n).argtypes = [P]
         getattr(L, n).restype = I
     L.fm_reset.argtypes = [P, P, P]

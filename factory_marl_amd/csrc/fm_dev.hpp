@@ -14,6 +14,7 @@ constexpr int MAXPC = 8;      // contacts per geom pair (box-box)
 
 // Flat per-arena record layouts (strides in elements)
 struct Dims {
+  static constexpr bool fixed = false;  // runtime dims (see FixedDims for compile-time scenes)
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -57,6 +58,7 @@ struct Model {
   const T* meaninertia;  // [N]
   const uint32_t* tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
+  int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one
 };
 
 template <typename T>
@@ -87,6 +89,26 @@ struct StepIO {
   const uint8_t* reset_mask;
 };
 
+// opaque copy of a pointer: loads through the result cannot be CSE'd with, or hoisted above, earlier
+// loads through the same pointer (keeps long-lived launch parameters out of the SGPR file)
+template <typename P>
+__device__ __forceinline__ const P* opaque(const P* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// LDS base with an opaque zero VGPR added: every workspace access becomes [vbase + immediate offset]
+// instead of one hoisted SGPR per distinct LDS address (which the compiler otherwise keeps live across
+// the whole substep loop and spills)
+__device__ __forceinline__ char* lds_base(char* smem) {
+#if FM_EXP_PLAINBASE
+  return smem;
+#endif
+  unsigned int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return smem + z;
+}
+
 // byte offsets of the per-arena LDS workspace (computed on the host, see lds_layout())
 struct Lay {
   int q, v, a, as, fs, fc, pb, g, dir, Ma, tmp, fa;
@@ -111,6 +133,7 @@ struct Lay {
   int uctl;   // double [nu]  clipped control of this env-step
   int scal;   // double [4]   per-step scalars broadcast from lane 0
   int prof;   // uint64 [16]  phase clocks of this arena (profiling only)
+  int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int total;
 };
 
@@ -198,5 +221,117 @@ __device__ __forceinline__ T wave_max(T x) {
   }
   return x;
 }
+
+template <typename T>
+struct StepParams {
+  Model<T> M;
+  State<T> S;
+  Lay L;
+  StepIO io;
+};
+
+// ------------------------------------------------------------------------------------------------
+// LDS workspace layout of one arena (byte offsets), shared by host and device.  For a compile-time
+// scene (FixedDims) every offset is a constant, so LDS accesses use immediate offsets off one
+// lane-address register instead of one address register per array.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
+                                              int maxrow, int ntree, int tsize) {
+  Lay L{};
+  int off = 0;
+  auto take = [&off](int bytes) {
+    int o = off;
+    off += (bytes + 15) & ~15;
+    return o;
+  };
+  // lane-broadcast row first: within ds_read2's 1 KiB offset reach of the workspace base
+  L.bc = take(tsize * WAVE);
+  L.q = take(tsize * nq);
+  L.v = take(tsize * nv);
+  L.a = take(tsize * nv);
+  L.as = take(tsize * nv);
+  L.fs = take(tsize * nv);
+  L.fc = take(tsize * nv);
+  L.pb = take(tsize * nv);
+  L.g = take(tsize * nv);
+  L.dir = take(tsize * nv);
+  L.Ma = take(tsize * nv);
+  L.tmp = take(tsize * nv);
+  L.fa = take(tsize * nv);
+  L.ctrl = take(8 * nu);
+  L.alen = take(tsize * nu);
+  L.avel = take(tsize * nu);
+  L.aforce = take(tsize * nu);
+  L.bpos = take(tsize * 30 * A);
+  L.bR = take(tsize * 90 * A);
+  L.bcom = take(tsize * 30 * A);
+  L.bIw = take(tsize * 60 * A);
+  L.bF = take(tsize * 30 * A);
+  L.bN = take(tsize * 30 * A);
+  L.dax = take(tsize * 27 * A);
+  L.danc = take(tsize * 27 * A);
+  L.site = take(tsize * 3 * A);
+  L.cR = take(tsize * 9 * K);
+  L.Marm = take(tsize * 81 * A);
+  L.ginfo = take(4 * ngc);
+  L.cbi = take(4 * 4 * ncb);
+  L.cbg = take(2 * ngc);
+  L.cube = take(tsize * 4 * K);
+  // phase-local buffers share one region: collision work lists (stage), the arm-block factor
+  // (smooth acceleration / integration) and the Newton Hessian (solve) are never live together
+  const int u0 = off;
+  L.H = take(tsize * nv * nv);
+  int uend = off;
+  off = u0;
+  L.gx = take(tsize * 4 * ngc);
+  L.cbw = take(tsize * 8 * ncb);
+  L.sp = take(4 * WAVE);
+  L.spoff = take(4 * WAVE);
+  L.gsurv = take(4 * 2 * WAVE);
+  L.stage = take(tsize * 8 * maxcon);
+  L.skey = take(4 * maxcon);
+  L.spw = take(4 * maxcon);
+  uend = off > uend ? off : uend;
+  off = u0;
+  L.Larm = take(tsize * 81 * A);
+  L.LBarm = L.Larm;
+  off = off > uend ? off : uend;
+  L.c_i = take(4 * 4 * maxcon);
+  L.c_r = take(tsize * CR_N * maxcon);
+  L.r_i = take(4 * 4 * maxrow);
+  L.r_r = take(tsize * RR_N * maxrow);
+  L.tmask = take(8 * ntree);
+  L.misc = take(4 * 16);
+  L.sort = take(4 * K);
+  L.uctl = take(8 * nu);
+  L.scal = take(8 * 4);
+  L.prof = take(8 * 16);
+  L.total = off;
+  return L;
+}
+
+// compile-time scene dimensions for the configurations the library specialises (A arms, K objects);
+// runtime-only quantities stay members
+template <int A_, int K_>
+struct FixedDims {
+  static constexpr bool fixed = true;
+  static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
+  static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
+  static constexpr int obs_dim = 24 * A_ + 13 * K_, act_dim = 8 * A_, maxrow = 10 * A_;
+  static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1, int_stride = 2 * K_ + I_NINT;
+  int N, nbox, npair, nparam, frame_skip, maxcon, ncbp;
+  __host__ __device__ FixedDims(const Dims& d)
+      : N(d.N), nbox(d.nbox), npair(d.npair), nparam(d.nparam), frame_skip(d.frame_skip), maxcon(d.maxcon),
+        ncbp(d.ncbp) {}
+  template <int TS>
+  __host__ __device__ static constexpr Lay layout() {
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXCON, maxrow, ntree, TS);
+  }
+  static bool matches(const Dims& d) {
+    return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&
+           d.ntree == ntree && d.obs_dim == obs_dim && d.act_dim == act_dim && d.maxrow == maxrow &&
+           d.phys_stride == phys_stride && d.dbl_stride == dbl_stride && d.int_stride == int_stride;
+  }
+};
 
 }  // namespace fm

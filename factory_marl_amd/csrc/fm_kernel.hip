@@ -20,6 +20,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -29,67 +30,447 @@
 #include "fm_dev.hpp"
 #include "fm_scene.hpp"
 
+#ifndef FM_WS_RUNTIME_LAYOUT
+#define FM_WS_RUNTIME_LAYOUT 0
+#endif
+// scenes with a compile-time specialised env-step kernel: X(num_arms, max_num_objects)
+#ifndef FM_FIXED_SCENES
+#define FM_FIXED_SCENES X(2, 4) X(2, 8) X(2, 10)
+#endif
+
 namespace fm {
 
 #define LANE ((int)threadIdx.x)
 #define SYNC() __syncthreads()
 
-template <typename T>
+template <typename T, typename DIM>
 struct Ws {
   char* base;
   const Lay* L;
-  __device__ T* q() const { return (T*)(base + L->q); }
-  __device__ T* v() const { return (T*)(base + L->v); }
-  __device__ T* a() const { return (T*)(base + L->a); }
-  __device__ T* as() const { return (T*)(base + L->as); }
-  __device__ T* fs() const { return (T*)(base + L->fs); }
-  __device__ T* fc() const { return (T*)(base + L->fc); }
-  __device__ T* pb() const { return (T*)(base + L->pb); }
-  __device__ T* g() const { return (T*)(base + L->g); }
-  __device__ T* dir() const { return (T*)(base + L->dir); }
-  __device__ T* Ma() const { return (T*)(base + L->Ma); }
-  __device__ T* tmp() const { return (T*)(base + L->tmp); }
-  __device__ T* fa() const { return (T*)(base + L->fa); }
-  __device__ double* ctrl() const { return (double*)(base + L->ctrl); }
-  __device__ T* alen() const { return (T*)(base + L->alen); }
-  __device__ T* avel() const { return (T*)(base + L->avel); }
-  __device__ T* aforce() const { return (T*)(base + L->aforce); }
-  __device__ T* bpos() const { return (T*)(base + L->bpos); }
-  __device__ T* bR() const { return (T*)(base + L->bR); }
-  __device__ T* bcom() const { return (T*)(base + L->bcom); }
-  __device__ T* bIw() const { return (T*)(base + L->bIw); }
-  __device__ T* bF() const { return (T*)(base + L->bF); }
-  __device__ T* bN() const { return (T*)(base + L->bN); }
-  __device__ T* dax() const { return (T*)(base + L->dax); }
-  __device__ T* danc() const { return (T*)(base + L->danc); }
-  __device__ T* site() const { return (T*)(base + L->site); }
-  __device__ T* cR() const { return (T*)(base + L->cR); }
-  __device__ T* Marm() const { return (T*)(base + L->Marm); }
-  __device__ T* Larm() const { return (T*)(base + L->Larm); }
-  __device__ T* LBarm() const { return (T*)(base + L->LBarm); }
-  __device__ T* gx() const { return (T*)(base + L->gx); }
-  __device__ int* ginfo() const { return (int*)(base + L->ginfo); }
-  __device__ int* cbi() const { return (int*)(base + L->cbi); }
-  __device__ T* cbw() const { return (T*)(base + L->cbw); }
-  __device__ uint16_t* cbg() const { return (uint16_t*)(base + L->cbg); }
-  __device__ uint32_t* sp() const { return (uint32_t*)(base + L->sp); }
-  __device__ int* spoff() const { return (int*)(base + L->spoff); }
-  __device__ uint32_t* gsurv() const { return (uint32_t*)(base + L->gsurv); }
-  __device__ T* stage() const { return (T*)(base + L->stage); }
-  __device__ int* skey() const { return (int*)(base + L->skey); }
-  __device__ uint32_t* spw() const { return (uint32_t*)(base + L->spw); }
-  __device__ T* cube() const { return (T*)(base + L->cube); }
-  __device__ T* H() const { return (T*)(base + L->H); }
-  __device__ int* ci() const { return (int*)(base + L->c_i); }
-  __device__ T* cr() const { return (T*)(base + L->c_r); }
-  __device__ int* ri() const { return (int*)(base + L->r_i); }
-  __device__ T* rr() const { return (T*)(base + L->r_r); }
-  __device__ uint64_t* tmask() const { return (uint64_t*)(base + L->tmask); }
-  __device__ int* misc() const { return (int*)(base + L->misc); }
-  __device__ int* sortidx() const { return (int*)(base + L->sort); }
-  __device__ double* uctl() const { return (double*)(base + L->uctl); }
-  __device__ double* scal() const { return (double*)(base + L->scal); }
-  __device__ unsigned long long* prof() const { return (unsigned long long*)(base + L->prof); }
+  __device__ __forceinline__ T* q() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.q);
+    } else {
+      return (T*)(base + L->q);
+    }
+  }
+  __device__ __forceinline__ T* v() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.v);
+    } else {
+      return (T*)(base + L->v);
+    }
+  }
+  __device__ __forceinline__ T* a() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.a);
+    } else {
+      return (T*)(base + L->a);
+    }
+  }
+  __device__ __forceinline__ T* as() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.as);
+    } else {
+      return (T*)(base + L->as);
+    }
+  }
+  __device__ __forceinline__ T* fs() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.fs);
+    } else {
+      return (T*)(base + L->fs);
+    }
+  }
+  __device__ __forceinline__ T* fc() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.fc);
+    } else {
+      return (T*)(base + L->fc);
+    }
+  }
+  __device__ __forceinline__ T* pb() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.pb);
+    } else {
+      return (T*)(base + L->pb);
+    }
+  }
+  __device__ __forceinline__ T* g() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.g);
+    } else {
+      return (T*)(base + L->g);
+    }
+  }
+  __device__ __forceinline__ T* dir() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.dir);
+    } else {
+      return (T*)(base + L->dir);
+    }
+  }
+  __device__ __forceinline__ T* Ma() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.Ma);
+    } else {
+      return (T*)(base + L->Ma);
+    }
+  }
+  __device__ __forceinline__ T* tmp() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.tmp);
+    } else {
+      return (T*)(base + L->tmp);
+    }
+  }
+  __device__ __forceinline__ T* fa() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.fa);
+    } else {
+      return (T*)(base + L->fa);
+    }
+  }
+  __device__ __forceinline__ double* ctrl() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (double*)(base + c.ctrl);
+    } else {
+      return (double*)(base + L->ctrl);
+    }
+  }
+  __device__ __forceinline__ T* alen() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.alen);
+    } else {
+      return (T*)(base + L->alen);
+    }
+  }
+  __device__ __forceinline__ T* avel() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.avel);
+    } else {
+      return (T*)(base + L->avel);
+    }
+  }
+  __device__ __forceinline__ T* aforce() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.aforce);
+    } else {
+      return (T*)(base + L->aforce);
+    }
+  }
+  __device__ __forceinline__ T* bpos() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bpos);
+    } else {
+      return (T*)(base + L->bpos);
+    }
+  }
+  __device__ __forceinline__ T* bR() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bR);
+    } else {
+      return (T*)(base + L->bR);
+    }
+  }
+  __device__ __forceinline__ T* bcom() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bcom);
+    } else {
+      return (T*)(base + L->bcom);
+    }
+  }
+  __device__ __forceinline__ T* bIw() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bIw);
+    } else {
+      return (T*)(base + L->bIw);
+    }
+  }
+  __device__ __forceinline__ T* bF() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bF);
+    } else {
+      return (T*)(base + L->bF);
+    }
+  }
+  __device__ __forceinline__ T* bN() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bN);
+    } else {
+      return (T*)(base + L->bN);
+    }
+  }
+  __device__ __forceinline__ T* dax() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.dax);
+    } else {
+      return (T*)(base + L->dax);
+    }
+  }
+  __device__ __forceinline__ T* danc() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.danc);
+    } else {
+      return (T*)(base + L->danc);
+    }
+  }
+  __device__ __forceinline__ T* site() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.site);
+    } else {
+      return (T*)(base + L->site);
+    }
+  }
+  __device__ __forceinline__ T* cR() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.cR);
+    } else {
+      return (T*)(base + L->cR);
+    }
+  }
+  __device__ __forceinline__ T* Marm() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.Marm);
+    } else {
+      return (T*)(base + L->Marm);
+    }
+  }
+  __device__ __forceinline__ T* Larm() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.Larm);
+    } else {
+      return (T*)(base + L->Larm);
+    }
+  }
+  __device__ __forceinline__ T* LBarm() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.LBarm);
+    } else {
+      return (T*)(base + L->LBarm);
+    }
+  }
+  __device__ __forceinline__ T* gx() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.gx);
+    } else {
+      return (T*)(base + L->gx);
+    }
+  }
+  __device__ __forceinline__ int* ginfo() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.ginfo);
+    } else {
+      return (int*)(base + L->ginfo);
+    }
+  }
+  __device__ __forceinline__ int* cbi() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.cbi);
+    } else {
+      return (int*)(base + L->cbi);
+    }
+  }
+  __device__ __forceinline__ T* cbw() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.cbw);
+    } else {
+      return (T*)(base + L->cbw);
+    }
+  }
+  __device__ __forceinline__ uint16_t* cbg() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (uint16_t*)(base + c.cbg);
+    } else {
+      return (uint16_t*)(base + L->cbg);
+    }
+  }
+  __device__ __forceinline__ uint32_t* sp() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (uint32_t*)(base + c.sp);
+    } else {
+      return (uint32_t*)(base + L->sp);
+    }
+  }
+  __device__ __forceinline__ int* spoff() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.spoff);
+    } else {
+      return (int*)(base + L->spoff);
+    }
+  }
+  __device__ __forceinline__ uint32_t* gsurv() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (uint32_t*)(base + c.gsurv);
+    } else {
+      return (uint32_t*)(base + L->gsurv);
+    }
+  }
+  __device__ __forceinline__ T* stage() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.stage);
+    } else {
+      return (T*)(base + L->stage);
+    }
+  }
+  __device__ __forceinline__ int* skey() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.skey);
+    } else {
+      return (int*)(base + L->skey);
+    }
+  }
+  __device__ __forceinline__ uint32_t* spw() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (uint32_t*)(base + c.spw);
+    } else {
+      return (uint32_t*)(base + L->spw);
+    }
+  }
+  __device__ __forceinline__ T* cube() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.cube);
+    } else {
+      return (T*)(base + L->cube);
+    }
+  }
+  __device__ __forceinline__ T* H() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.H);
+    } else {
+      return (T*)(base + L->H);
+    }
+  }
+  __device__ __forceinline__ int* ci() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.c_i);
+    } else {
+      return (int*)(base + L->c_i);
+    }
+  }
+  __device__ __forceinline__ T* cr() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.c_r);
+    } else {
+      return (T*)(base + L->c_r);
+    }
+  }
+  __device__ __forceinline__ int* ri() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.r_i);
+    } else {
+      return (int*)(base + L->r_i);
+    }
+  }
+  __device__ __forceinline__ T* rr() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.r_r);
+    } else {
+      return (T*)(base + L->r_r);
+    }
+  }
+  __device__ __forceinline__ uint64_t* tmask() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (uint64_t*)(base + c.tmask);
+    } else {
+      return (uint64_t*)(base + L->tmask);
+    }
+  }
+  __device__ __forceinline__ int* misc() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.misc);
+    } else {
+      return (int*)(base + L->misc);
+    }
+  }
+  __device__ __forceinline__ int* sortidx() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (int*)(base + c.sort);
+    } else {
+      return (int*)(base + L->sort);
+    }
+  }
+  __device__ __forceinline__ double* uctl() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (double*)(base + c.uctl);
+    } else {
+      return (double*)(base + L->uctl);
+    }
+  }
+  __device__ __forceinline__ double* scal() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (double*)(base + c.scal);
+    } else {
+      return (double*)(base + L->scal);
+    }
+  }
+  __device__ __forceinline__ T* bc() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.bc);
+    } else {
+      return (T*)(base + L->bc);
+    }
+  }
+  __device__ __forceinline__ unsigned long long* prof() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (unsigned long long*)(base + c.prof);
+    } else {
+      return (unsigned long long*)(base + L->prof);
+    }
+  }
 };
 
 // optional phase profile: lane 0 charges the wall-clock time since the previous mark to phase k
@@ -109,17 +490,21 @@ struct Ws {
 // ------------------------------------------------------------------------------------------------
 // tree / dof helpers
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int tree_dof(const Dims& d, int t) {
+template <typename DD>
+__device__ __forceinline__ int tree_dof(const DD& d, int t) {
   return t == 0 ? 0 : (t <= d.K ? 1 + 6 * (t - 1) : 1 + 6 * d.K + 9 * (t - 1 - d.K));
 }
-__device__ __forceinline__ int tree_nd(const Dims& d, int t) { return t == 0 ? 1 : (t <= d.K ? 6 : 9); }
-__device__ __forceinline__ int kbody_tree(const Dims& d, int kb) {
+template <typename DD>
+__device__ __forceinline__ int tree_nd(const DD& d, int t) { return t == 0 ? 1 : (t <= d.K ? 6 : 9); }
+template <typename DD>
+__device__ __forceinline__ int kbody_tree(const DD& d, int kb) {
   if (kb == 0) return -1;
   if (kb == 1) return 0;
   if (kb < 2 + d.K) return kb - 1;
   return 1 + d.K + (kb - 2 - d.K) / 10;
 }
-__device__ __forceinline__ int dof_tree(const Dims& d, int i) {
+template <typename DD>
+__device__ __forceinline__ int dof_tree(const DD& d, int i) {
   if (i == 0) return 0;
   if (i < 1 + 6 * d.K) return 1 + (i - 1) / 6;
   return 1 + d.K + (i - 1 - 6 * d.K) / 9;
@@ -492,9 +877,9 @@ __device__ __forceinline__ void np_box_box(const T* p1, const T* R1, const T* h1
 //   4. narrowphase per geom pair (one pair per lane), contacts staged with LDS atomics
 //   5. staged contacts sorted by (geom pair, index) into the contact slots
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void geom_frame(const Model<T>& M, const Ws<T>& w, int g, int kb, T* R, T* h) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void geom_frame(const Model<T>& M, const Ws<T, DIM>& w, int g, int kb, T* R, T* h) {
+  const DIM dm(M.dm);
   const T* gg = M.geom + 16 * g;
   if (kb >= 2 && kb < 2 + dm.K) {
     const T* c = w.cR() + 9 * (kb - 2);
@@ -519,9 +904,9 @@ __device__ __forceinline__ void geom_frame(const Model<T>& M, const Ws<T>& w, in
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T>& w, const uint32_t* list, int n) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>& w, const uint32_t* list, int n) {
+  const DIM dm(M.dm);
   if (LANE >= n) return;
   uint32_t pwd = list[LANE];
   int c1 = pwd & 4095, c2 = (pwd >> 12) & 4095;
@@ -557,9 +942,9 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T>& w, 
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void collide(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
+  const DIM dm(M.dm);
   const int K = dm.K;
   const T* q = w.q();
   T* gx = w.gx();
@@ -567,12 +952,17 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T>& w, int a
   const int* cbi = w.cbi();
   int* misc = w.misc();
   const uint64_t below = (1ull << LANE) - 1ull;
-  // 1. moving geom centres (static ones were written at launch)
+  // 1. geom centres + rbound (the buffer is phase-local, so static geoms are rewritten too)
   for (int g = LANE; g < dm.ngc; g += WAVE) {
-    int kb = (gin[g] >> 8) & 255;
-    if (kb == 0) continue;
+    const int kb = (gin[g] >> 8) & 255;
+    const T* gg = M.geom + 16 * g;
     T* o = gx + 4 * g;
-    if (kb == 1) {
+    o[3] = gg[15];
+    if (kb == 0) {
+      o[0] = gg[0];
+      o[1] = gg[1];
+      o[2] = gg[2];
+    } else if (kb == 1) {
       o[0] = 0;
       o[1] = q[0];
       o[2] = T(1.05);
@@ -583,7 +973,6 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T>& w, int a
       o[2] = c[2];
     } else {
       int arm = (kb - 2 - K) / 10, b = (kb - 2 - K) % 10;
-      const T* gg = M.geom + 16 * g;
       const T* bp = w.bpos() + 30 * arm + 3 * b;
       const T* bR = w.bR() + 90 * arm + 9 * b;
       T off[3];
@@ -596,10 +985,15 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T>& w, int a
   // 2. collision-body bounds
   for (int b = LANE; b < dm.ncb; b += WAVE) {
     const int kb = cbi[4 * b], fl = cbi[4 * b + 1];
-    if (fl & CB_STATIC) continue;
     T* o = w.cbw() + 8 * b;
-    if (kb == 1) {
+    const T* cs = M.cbs + 8 * b;
+#pragma unroll
+    for (int k = 0; k < 7; k++) o[k] = cs[k];
+    if (fl & CB_STATIC) {
+    } else if (kb == 1) {
+      o[0] = T(0);
       o[1] = q[0];
+      o[2] = T(1.05);
     } else if (kb < 2 + K) {
       const T* c = q + 1 + 7 * (kb - 2);
       o[0] = c[0];
@@ -748,9 +1142,9 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T>& w, int a
 // ------------------------------------------------------------------------------------------------
 // stage (mj_step1): kinematics, inertia, bias forces, collision, constraint rows, efc velocities
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T>& w, int arm, bool with_dyn) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w, int arm, bool with_dyn) {
+  const DIM dm(M.dm);
   const T* q = w.q() + 1 + 7 * dm.K + 9 * arm;
   const T* qd = w.v() + 1 + 6 * dm.K + 9 * arm;
   const T* base = M.arm_base + 12 * arm;
@@ -938,8 +1332,8 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T>& w, int
 }
 
 // column of the translational Jacobian of point p on arm body b for arm dof d (0 if not in chain)
-template <typename T>
-__device__ __forceinline__ void arm_jac_col(const Ws<T>& w, int arm, int b, int d, const T* p, T* col) {
+template <typename T, typename DIM>
+__device__ __forceinline__ void arm_jac_col(const Ws<T, DIM>& w, int arm, int b, int d, const T* p, T* col) {
   const T* ax = w.dax() + 27 * arm + 3 * d;
   bool in = d < 7 ? (b >= 7 || d <= b) : ((d == 7 && b == 8) || (d == 8 && b == 9));
   if (!in) {
@@ -958,9 +1352,9 @@ __device__ __forceinline__ void arm_jac_col(const Ws<T>& w, int arm, int b, int 
 }
 
 // translational Jacobian column j (tree-local) of point p on kernel body kb in its tree
-template <typename T>
-__device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T>& w, int kb, int j, const T* p, T* col) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T, DIM>& w, int kb, int j, const T* p, T* col) {
+  const DIM dm(M.dm);
   if (kb == 1) {
     col[0] = 0;
     col[1] = 1;
@@ -983,9 +1377,9 @@ __device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T>& w, 
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void stage(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
+  const DIM dm(M.dm);
   const int A = dm.A, K = dm.K, nv = dm.nv;
   T* q = w.q();
   T* v = w.v();
@@ -1243,8 +1637,8 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T>& w, int are
 // ------------------------------------------------------------------------------------------------
 // block-diagonal M products and solves (belt scalar, cubes diagonal, arm 9x9 blocks)
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ T Mdiag(const Model<T>& M, const Ws<T>& w, int i) {
+template <typename T, typename DIM>
+__device__ __forceinline__ T Mdiag(const Model<T>& M, const Ws<T, DIM>& w, int i) {
   if (i == 0) return M.belt_mass;
   int k = (i - 1) / 6, r = (i - 1) % 6;
   const T* c = w.cube() + 4 * k;
@@ -1252,9 +1646,9 @@ __device__ __forceinline__ T Mdiag(const Model<T>& M, const Ws<T>& w, int i) {
 }
 
 // out = M x   (lanes over dofs)
-template <typename T>
-__device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T>& w, int arena, const T* x, T* out) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T, DIM>& w, int arena, const T* x, T* out) {
+  const DIM dm(M.dm);
   int a0 = 1 + 6 * dm.K;
   for (int i = LANE; i < dm.nv; i += WAVE) {
     if (i < a0) {
@@ -1300,6 +1694,79 @@ __device__ __forceinline__ void cholsolve9(const T* L, T* x) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// register-resident dense Cholesky + solve of H dir = -g for nv <= NVM (lane j holds column j of the
+// symmetric matrix in NVM registers; pivots and multipliers are broadcast with v_readlane)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float readlane(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+__device__ __forceinline__ double readlane(double x, int l) {
+  long long b = __double_as_longlong(x);
+  int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ float lane_bcast(float x, int l) { return readlane(x, l); }
+__device__ __forceinline__ double lane_bcast(double x, int l) { return __shfl(x, l); }
+
+template <typename T, int NVM>
+__device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const T* g, T* dir) {
+  const int j = LANE;
+  const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
+  T col[NVM];
+#pragma unroll
+  for (int i = 0; i < NVM; i++) col[i] = (i < nv && j < nv) ? H[i * nv + j] : T(0);
+  SYNC();
+  T dinv = T(1);
+  // factor: after step k lane j (> k) holds L[j][k] in col[k]; lane k holds L[k][k]; lane j's entries
+  // col[i], i > j, keep L[i][j] * L[j][j].  Rows >= nv are zero, so updates need no row guard.
+#pragma unroll
+  for (int k = 0; k < NVM; k++) {
+    if (k < nv) {
+      bc[j] = col[k];  // row k of the trailing matrix (= column k by symmetry)
+      SYNC();
+      T d = bc[k];
+      d = d > tiny ? d : tiny;
+      const T ri = T(1) / sqrt(d);
+      const T lj = col[k] * ri;
+      if (j == k) dinv = ri;
+      if (j >= k) col[k] = lj;
+      if (j > k) {
+        const T s = lj * ri;
+#pragma unroll
+        for (int i = k + 1; i < NVM; i++) col[i] -= bc[i] * s;
+      }
+      SYNC();
+    }
+  }
+  // forward: L y = -g ; y_k is formed on lane k and broadcast (v_readlane for fp32; ds_bpermute for
+  // fp64, whose split 64-bit v_readlane miscompiles in the fully unrolled fixed-size kernel)
+  T acc = j < nv ? -g[j] : T(0);
+  T y = T(0);
+#pragma unroll
+  for (int k = 0; k < NVM; k++) {
+    if (k < nv) {
+      const T yk = lane_bcast(acc * dinv, k);
+      if (j == k) y = yk;
+      if (j > k) acc -= col[k] * yk;
+    }
+  }
+  // backward: L' x = y
+  T acc2 = y, x = T(0);
+#pragma unroll
+  for (int k = NVM - 1; k >= 0; k--) {
+    if (k < nv) {
+      const T xk = lane_bcast(acc2 * dinv, k);
+      if (j == k) x = xk;
+      if (j < k) acc2 -= col[k] * dinv * xk;
+    }
+  }
+  if (j < nv) dir[j] = x;
+  SYNC();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Newton solver on the primal cost (see oracle/solver.c for the definition)
 // ------------------------------------------------------------------------------------------------
 template <typename T>
@@ -1308,9 +1775,9 @@ __device__ __forceinline__ T edge_val(const T* x3, T mu, int e) {
 }
 
 // evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
-template <typename T>
-__device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T>& w, const T* x, int ncon, int nrow) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T, DIM>& w, const T* x, int ncon, int nrow) {
+  const DIM dm(M.dm);
   T cst = 0;
   for (int c = LANE; c < ncon; c += WAVE) {
     const int* ci = w.ci() + 4 * c;
@@ -1347,8 +1814,8 @@ __device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T>& w, const 
 }
 
 // f3 (per contact, stored in CR_F[0..2]) = D * sum_active jar_e c_e ; used for gradient / forces
-template <typename T>
-__device__ __forceinline__ void contact_f3(const Ws<T>& w, int ncon) {
+template <typename T, typename DIM>
+__device__ __forceinline__ void contact_f3(const Ws<T, DIM>& w, int ncon) {
   for (int c = LANE; c < ncon; c += WAVE) {
     T* cr = w.cr() + CR_N * c;
     T mu = cr[CR_MU], D = cr[CR_D];
@@ -1373,9 +1840,9 @@ __device__ __forceinline__ void contact_f3(const Ws<T>& w, int ncon) {
 }
 
 // out_i = sum over rows of J_ri * (D jar)_r for active rows  (constraint part of the gradient)
-template <typename T>
-__device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T>& w, int ncon, int nrow, T* out, bool add) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, T* out, bool add) {
+  const DIM dm(M.dm);
   for (int i = LANE; i < dm.nv; i += WAVE) {
     int t = dof_tree(dm, i);
     int jl = i - tree_dof(dm, t);
@@ -1404,9 +1871,9 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T>& w, in
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void newton(const Model<T>& M, const Ws<T>& w, int arena, int64_t* ctr) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
+  const DIM dm(M.dm);
   const int nv = dm.nv;
   const int ncon = w.misc()[MISC_NCON], nrow = w.misc()[MISC_NROW];
   T* a = w.a();
@@ -1528,42 +1995,50 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T>& w, int ar
     }
     SYNC();
     PMARK(PH_NHESS);
-    // dense Cholesky (right-looking over the column-major lower-triangle table)
-    int colstart = 0;
-    for (int k = 0; k < nv; k++) {
-      if (LANE == 0) {
-        T s = H[k * nv + k];
-        H[k * nv + k] = sqrt(s > T(1e-300) ? s : T(1e-300));
+    if (nv <= 48 && !(M.dbg_flags & 1)) {
+      chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
+      PMARK(PH_NCHOL);
+    } else if (nv <= 64 && !(M.dbg_flags & 1)) {
+      chol_solve_reg<T, 64>(H, w.bc(), nv, g, dir);
+      PMARK(PH_NCHOL);
+    } else {
+      // dense Cholesky (right-looking over the column-major lower-triangle table)
+      int colstart = 0;
+      for (int k = 0; k < nv; k++) {
+        if (LANE == 0) {
+          T s = H[k * nv + k];
+          H[k * nv + k] = sqrt(s > T(1e-300) ? s : T(1e-300));
+        }
+        SYNC();
+        T lkk = H[k * nv + k];
+        for (int i = k + 1 + LANE; i < nv; i += WAVE) H[i * nv + k] /= lkk;
+        SYNC();
+        colstart += nv - k;  // start of column k+1 in the table
+        for (int e = colstart + LANE; e < ntri; e += WAVE) {
+          uint32_t ij = M.tri[e];
+          int i = ij & 0xFFFF, j = ij >> 16;
+          H[i * nv + j] -= H[i * nv + k] * H[j * nv + k];
+        }
+        SYNC();
       }
+      PMARK(PH_NCHOL);
+      // dir = -H^-1 g  (column-oriented substitutions)
+      for (int i = LANE; i < nv; i += WAVE) dir[i] = -g[i];
       SYNC();
-      T lkk = H[k * nv + k];
-      for (int i = k + 1 + LANE; i < nv; i += WAVE) H[i * nv + k] /= lkk;
-      SYNC();
-      colstart += nv - k;  // start of column k+1 in the table
-      for (int e = colstart + LANE; e < ntri; e += WAVE) {
-        uint32_t ij = M.tri[e];
-        int i = ij & 0xFFFF, j = ij >> 16;
-        H[i * nv + j] -= H[i * nv + k] * H[j * nv + k];
+      for (int k = 0; k < nv; k++) {
+        T xk = dir[k] / H[k * nv + k];
+        SYNC();
+        if (LANE == 0) dir[k] = xk;
+        for (int i = k + 1 + LANE; i < nv; i += WAVE) dir[i] -= H[i * nv + k] * xk;
+        SYNC();
       }
-      SYNC();
-    }
-    PMARK(PH_NCHOL);
-    // dir = -H^-1 g  (column-oriented substitutions)
-    for (int i = LANE; i < nv; i += WAVE) dir[i] = -g[i];
-    SYNC();
-    for (int k = 0; k < nv; k++) {
-      T xk = dir[k] / H[k * nv + k];
-      SYNC();
-      if (LANE == 0) dir[k] = xk;
-      for (int i = k + 1 + LANE; i < nv; i += WAVE) dir[i] -= H[i * nv + k] * xk;
-      SYNC();
-    }
-    for (int k = nv - 1; k >= 0; k--) {
-      T xk = dir[k] / H[k * nv + k];
-      SYNC();
-      if (LANE == 0) dir[k] = xk;
-      for (int i = LANE; i < k; i += WAVE) dir[i] -= H[k * nv + i] * xk;
-      SYNC();
+      for (int k = nv - 1; k >= 0; k--) {
+        T xk = dir[k] / H[k * nv + k];
+        SYNC();
+        if (LANE == 0) dir[k] = xk;
+        for (int i = LANE; i < k; i += WAVE) dir[i] -= H[k * nv + i] * xk;
+        SYNC();
+      }
     }
     PMARK(PH_NSOLVE);
     // exact line search along dir (segment walking over the breakpoints of the inequality rows)
@@ -1690,9 +2165,9 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T>& w, int ar
 // ------------------------------------------------------------------------------------------------
 // step2: actuation, smooth acceleration, constraint solve, implicitfast integration
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T, DIM>& w, int arena, bool actuation) {
+  const DIM dm(M.dm);
   const int K = dm.K, nv = dm.nv;
   T* fa = w.fa();
   for (int i = LANE; i < nv; i += WAVE) fa[i] = T(0);
@@ -1742,9 +2217,9 @@ __device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T>& w, in
   SYNC();
 }
 
-template <typename T>
-__device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T>& w, int arena, bool actuation) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T, DIM>& w, int arena, bool actuation) {
+  const DIM dm(M.dm);
   const int K = dm.K, nv = dm.nv;
   const T dt = M.dt;
   T* q = w.q();
@@ -1846,8 +2321,8 @@ __device__ __forceinline__ double pcg_double(uint64_t* st) {
   return (double)(pcg_next(st) >> 11) * (1.0 / 9007199254740992.0);
 }
 
-template <typename T>
-__device__ __forceinline__ void hide_cube(const Dims& dm, T* q, T* v, int32_t* ti, int obj) {
+template <typename T, typename DD>
+__device__ __forceinline__ void hide_cube(const DD& dm, T* q, T* v, int32_t* ti, int obj) {
   ti[dm.K + ti[2 * dm.K + I_NOUT]] = obj;
   ti[2 * dm.K + I_NOUT]++;
   T* qq = q + 1 + 7 * obj;
@@ -1868,9 +2343,9 @@ __device__ __forceinline__ void pop_at(int32_t* list, int32_t* n, int idx) {
 }
 
 // TaskManager.reset (task_utils.py:146-156) + BaseEnv.reset_sim bits (base_env.py:184-190)
-template <typename T>
+template <typename T, typename DIM>
 __device__ __forceinline__ void task_reset(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, double* ctrl) {
-  const Dims& dm = M.dm;
+  const DIM dm(M.dm);
   const int K = dm.K;
   for (int k = 0; k < K; k++) {
     T* qq = q + 1 + 7 * k;
@@ -1896,9 +2371,9 @@ __device__ __forceinline__ void task_reset(const Model<T>& M, T* q, T* v, int32_
   td[2] = 0.0;            // play_time
 }
 
-template <typename T>
+template <typename T, typename DIM>
 __device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr) {
-  const Dims& dm = M.dm;
+  const DIM dm(M.dm);
   const int K = dm.K;
   int32_t* ins = ti;
   int32_t* outs = ti + K;
@@ -1965,13 +2440,13 @@ __device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t*
 // in-scene cubes sorted by x (stable), zero padded: poses K x 7, velocities K x 6
 // lane 0: TaskManager.step, BaseEnv.step_sim bookkeeping (base_env.py:266-270), progress / score reward
 // (environments.py:129-149, 342-383), Monitor episode return; results in w.scal()
-template <typename T>
-__device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T>& w, int32_t* ti, double* td, uint64_t* rng,
+template <typename T, typename DIM>
+__device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td, uint64_t* rng,
                                        int64_t* ctr, const float* act) {
-  const Dims& dm = M.dm;
+  const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
   double* sc = w.scal();
-  int fail = task_step(M, w.q(), w.v(), ti, td, rng, ctr);
+  int fail = task_step<T, DIM>(M, w.q(), w.v(), ti, td, rng, ctr);
   double dt_env = 0.001 * dm.frame_skip;
   td[2] += dt_env;
   td[1] += M.accel * dt_env;
@@ -2026,9 +2501,9 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T>& w, int
   ts[I_EPLEN]++;
 }
 
-template <typename T>
-__device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T>& w, const int32_t* ti, float* obs) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w, const int32_t* ti, float* obs) {
+  const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
   const T* q = w.q();
   const T* v = w.v();
@@ -2073,9 +2548,9 @@ __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T>& w, con
 // ------------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena, bool stage_copy) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T, DIM>& w, int arena, bool stage_copy) {
+  const DIM dm(M.dm);
   const T* ph = S.phys + (size_t)arena * dm.phys_stride;
   const T* src_q = ph + (stage_copy ? dm.nq + dm.nv : 0);
   const T* src_v = ph + dm.nq + (stage_copy ? dm.nq + dm.nv : 0);
@@ -2084,38 +2559,21 @@ __device__ __forceinline__ void load_state(const Model<T>& M, const State<T>& S,
 }
 
 // per-launch LDS setup: geom / collision-body tables, static geom centres, body bounds, cube sizes
-template <typename T>
-__device__ __forceinline__ void init_arena(const Model<T>& M, const Ws<T>& w, int arena) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void init_arena(const Model<T>& M, const Ws<T, DIM>& w, int arena) {
+  const DIM dm(M.dm);
   for (int g = LANE; g < dm.ngc; g += WAVE) {
-    const int gi = M.ginfo[g];
-    w.ginfo()[g] = gi;
-    const T* gg = M.geom + 16 * g;
-    T* o = w.gx() + 4 * g;
-    const int kb = (gi >> 8) & 255;
-    if (kb == 0) {
-      o[0] = gg[0];
-      o[1] = gg[1];
-      o[2] = gg[2];
-    }
-    o[3] = gg[15];
+    w.ginfo()[g] = M.ginfo[g];
     w.cbg()[g] = M.cbg[g];
   }
-  for (int b = LANE; b < dm.ncb; b += WAVE) {
-    for (int k = 0; k < 4; k++) w.cbi()[4 * b + k] = M.cbi[4 * b + k];
-    for (int k = 0; k < 8; k++) w.cbw()[8 * b + k] = M.cbs[8 * b + k];
-    if (M.cbi[4 * b] == 1) {  // belt AABB: x, z fixed
-      w.cbw()[8 * b] = T(0);
-      w.cbw()[8 * b + 2] = T(1.05);
-    }
-  }
+  for (int i = LANE; i < 4 * dm.ncb; i += WAVE) w.cbi()[i] = M.cbi[i];
   for (int i = LANE; i < 4 * dm.K; i += WAVE) w.cube()[i] = M.cube[(size_t)arena * dm.K * 4 + i];
 }
 
 // physics.reset() + TaskManager.reset() + after_reset forward (actuation disabled) -> warmstart
-template <typename T>
-__device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T>& w, int arena, int32_t* ti, double* td, int64_t* ctr) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T, DIM>& w, int arena, int32_t* ti, double* td, int64_t* ctr) {
+  const DIM dm(M.dm);
   T* q = w.q();
   T* v = w.v();
   for (int i = LANE; i < dm.nq; i += WAVE) q[i] = T(0);
@@ -2124,7 +2582,7 @@ __device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T>& w, i
     w.a()[i] = T(0);
   }
   SYNC();
-  if (LANE == 0) task_reset(M, q, v, ti, td, w.ctrl());
+  if (LANE == 0) task_reset<T, DIM>(M, q, v, ti, td, w.ctrl());
   SYNC();
   stage(M, w, arena, ctr);
   smooth_acc(M, w, arena, false);
@@ -2136,9 +2594,9 @@ __device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T>& w, i
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S, const Ws<T>& w, int arena) {
-  const Dims& dm = M.dm;
+template <typename T, typename DIM>
+__device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S, const Ws<T, DIM>& w, int arena) {
+  const DIM dm(M.dm);
   T* ph = S.phys + (size_t)arena * dm.phys_stride;
   for (int i = LANE; i < dm.nq; i += WAVE) ph[i] = w.q()[i];
   for (int i = LANE; i < dm.nv; i += WAVE) ph[dm.nq + i] = w.v()[i];
@@ -2147,13 +2605,13 @@ __device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S
   for (int u = LANE; u < dm.nu; u += WAVE) db[u] = w.ctrl()[u];
 }
 
-template <typename T>
+template <typename T, typename DIM>
 __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L, float* obs, const uint8_t* mask) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int arena = blockIdx.x;
-  const Dims& dm = M.dm;
+  const DIM dm(M.dm);
   if (mask && !mask[arena]) return;
-  Ws<T> w{smem, &L};
+  Ws<T, DIM> w{lds_base(smem), &L};
   int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
   double* td = S.dbl + (size_t)arena * dm.dbl_stride + dm.nu;
   int64_t* ctr = S.counters + 4 * (size_t)arena;
@@ -2173,29 +2631,39 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   if (obs) write_obs(M, w, ti, obs + (size_t)arena * dm.obs_dim);
 }
 
-template <typename T>
-__global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L, StepIO io) {
+template <typename T, typename DIM>
+__global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  (void)params;
+  // All launch parameters are read through an opaque pointer to the kernarg segment at each use, so the
+  // compiler cannot hoist the ~50 scalar values out of the substep loop and run out of SGPRs.
+  const StepParams<T>* PK = (const StepParams<T>*)__builtin_amdgcn_kernarg_segment_ptr();
+#define M (opaque(PK)->M)
+#define S (opaque(PK)->S)
+#define io (opaque(PK)->io)
+#define L (opaque(PK)->L)
   const int arena = blockIdx.x;
-  const Dims& dm = M.dm;
+  const DIM dm(M.dm);
   const int A = dm.A, K = dm.K, nu = dm.nu;
-  Ws<T> w{smem, &L};
+  // a fresh opaque LDS base per use: workspace addresses are recomputed inside each phase instead of
+  // being hoisted out of the substep loop (which would keep every phase's addresses live everywhere)
+#define w (Ws<T, DIM>{lds_base(smem), &L})
   if (M.prof && LANE < 16) w.prof()[LANE] = LANE == PH_LAST ? wall_clock64() : 0ull;
-  int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
-  double* td = S.dbl + (size_t)arena * dm.dbl_stride + nu;  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
-  uint64_t* rng = S.rng + 4 * (size_t)arena;
-  int64_t* ctr = S.counters + 4 * (size_t)arena;
-  const float* act = io.actions + (size_t)arena * dm.act_dim;
+#define ti (S.ints + (size_t)arena * dm.int_stride)
+#define td (S.dbl + (size_t)arena * dm.dbl_stride + nu)  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
+#define rng (S.rng + 4 * (size_t)arena)
+#define ctr (S.counters + 4 * (size_t)arena)
+#define act (io.actions + (size_t)arena * dm.act_dim)
   // ---- ctrl_target (double) and the clipped AllFullRL control (environments.py:84-102, base_env.py:255-262)
-  double* ctrl = w.ctrl();
+#define ctrl_ (w.ctrl())
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
-  for (int u = LANE; u < nu; u += WAVE) ctrl[u] = dsrc[u];
-  double speed = td[1];
-  double* uctl = w.uctl();
+  for (int u = LANE; u < nu; u += WAVE) ctrl_[u] = dsrc[u];
+  const double speed0 = td[1];
+#define uctl_ (w.uctl())
   for (int u = LANE; u < nu; u += WAVE) {
     double c;
     if (u == 0) {
-      c = speed;
+      c = speed0;
     } else {
       int j = (u - 1) % 8;
       float a = (float)tanh((double)act[u - 1]);  // correctly rounded float32 tanh (np.tanh on float32)
@@ -2204,7 +2672,7 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
       c = lo + (double)s * (hi - lo);
     }
     double lo = (double)M.ctrlrange[2 * u], hi = (double)M.ctrlrange[2 * u + 1];
-    uctl[u] = c < lo ? lo : (c > hi ? hi : c);
+    uctl_[u] = c < lo ? lo : (c > hi ? hi : c);
   }
   init_arena(M, w, arena);
   // warmstart
@@ -2214,9 +2682,9 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
   // stage (mj_step1) at the state of the last mj_step1 (pre-teleport), then integrate the current state
   load_state(M, S, w, arena, true);
   SYNC();
-  const double lp = 0.001 / (0.001 + M.pt_time);
-  T* phw = S.phys + (size_t)arena * dm.phys_stride;
-  double* sc = w.scal();  // [0] reward, [1] terminated, [2] out_of_reach, [3] force_terminate
+#define lp (0.001 / (0.001 + M.pt_time))
+#define phw (S.phys + (size_t)arena * dm.phys_stride)
+#define sc_ (w.scal())  // [0] reward, [1] terminated, [2] out_of_reach, [3] force_terminate
   bool reset_pass = false;
   // Every physics phase has exactly one call site (the kernel is one loop), which keeps the code that a
   // substep walks through small enough for the instruction cache:
@@ -2230,8 +2698,8 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
     }
     if (!reset_pass) {
       for (int u = LANE; u < nu; u += WAVE) {
-        double ct = ctrl[u] + (uctl[u] - ctrl[u]) * lp;
-        ctrl[u] = u == 0 ? -speed : ct;
+        double ct = ctrl_[u] + (uctl_[u] - ctrl_[u]) * lp;
+        ctrl_[u] = u == 0 ? -td[1] : ct;
       }
       SYNC();
     }
@@ -2265,7 +2733,7 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
         mx = fabs(f2) > mx ? fabs(f2) : mx;
         if ((double)mx > M.force_thr) hit = true;
       }
-      if (LANE == 0) sc[3] = __ballot(hit) != 0ull ? 1.0 : 0.0;
+      if (LANE == 0) sc_[3] = __ballot(hit) != 0ull ? 1.0 : 0.0;
     }
     // gripper sites at the final state (the last mj_step1's site_xpos)
     if (LANE < A) arm_chain(M, w, LANE, false);
@@ -2275,12 +2743,12 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
     for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
     if (LANE == 0) task_tail(M, w, ti, td, rng, ctr, act);
     SYNC();
-    const int term = sc[1] != 0.0;
+    const int term = sc_[1] != 0.0;
     if (LANE == 0) {
-      const int s_fail = sc[2] != 0.0;
-      const bool force_term = sc[3] != 0.0;
+      const int s_fail = sc_[2] != 0.0;
+      const bool force_term = sc_[3] != 0.0;
       int32_t* ts = ti + 2 * K;
-      if (io.reward) io.reward[arena] = (float)sc[0];
+      if (io.reward) io.reward[arena] = (float)sc_[0];
       if (io.terminated) io.terminated[arena] = (uint8_t)term;
       if (io.truncated) io.truncated[arena] = 0;
       if (io.scores) {
@@ -2313,7 +2781,7 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
     }
     SYNC();
     if (LANE == 0) {
-      task_reset(M, w.q(), w.v(), ti, td, w.ctrl());
+      task_reset<T, DIM>(M, w.q(), w.v(), ti, td, w.ctrl());
       td[3 + 2 * A] = 0.0;
       ti[2 * K + I_EPLEN] = 0;
     }
@@ -2326,6 +2794,21 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
   if (io.obs) write_obs(M, w, ti, io.obs + (size_t)arena * dm.obs_dim);
   PMARK(PH_TAIL);
   if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);
+#undef ctrl_
+#undef uctl_
+#undef sc_
+#undef w
+#undef M
+#undef S
+#undef io
+#undef L
+#undef ti
+#undef td
+#undef rng
+#undef ctr
+#undef act
+#undef phw
+#undef lp
 }
 
 
@@ -2333,12 +2816,12 @@ __global__ void __launch_bounds__(64) step_kernel(Model<T> M, State<T> S, Lay L,
 // internals (float64) for comparison with the oracle.  Layout (see fm_debug_dump in the C ABI):
 // [0] ncon [1] nrow | Marm A*81 | pb nv | as nv | a nv | fc nv | site 3A | bpos 30A | bcom 30A |
 // dax 27A | contacts 64 x (g1 g2 dist pos3 frame9 mu D) | rows 20A x (d0 d1 pos D aref f)
-template <typename T>
+template <typename T, typename DIM>
 __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L, int arena, int actuated,
                                                    double* out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Dims& dm = M.dm;
-  Ws<T> w{smem, &L};
+  const DIM dm(M.dm);
+  Ws<T, DIM> w{lds_base(smem), &L};
   int64_t* ctr = S.counters + 4 * (size_t)arena;
   const T* ph = S.phys + (size_t)arena * dm.phys_stride;
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
@@ -2468,6 +2951,8 @@ struct fm_handle {
   int64_t* counters = nullptr;
   unsigned long long* prof = nullptr;
   bool prof_on = false;
+  int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
+  Lay lay_step{};  // workspace layout of the env-step kernel in use
 };
 
 template <typename T>
@@ -2491,68 +2976,7 @@ static int upload_raw(fm_handle* h, U** dst, const std::vector<U>& src) {
 }
 
 static Lay lds_layout(const Dims& d, int tsize) {
-  Lay L;
-  int off = 0;
-  auto take = [&](int bytes) {
-    int o = off;
-    off += (bytes + 15) & ~15;
-    return o;
-  };
-  int nv = d.nv, A = d.A, K = d.K;
-  L.q = take(tsize * d.nq);
-  L.v = take(tsize * nv);
-  L.a = take(tsize * nv);
-  L.as = take(tsize * nv);
-  L.fs = take(tsize * nv);
-  L.fc = take(tsize * nv);
-  L.pb = take(tsize * nv);
-  L.g = take(tsize * nv);
-  L.dir = take(tsize * nv);
-  L.Ma = take(tsize * nv);
-  L.tmp = take(tsize * nv);
-  L.fa = take(tsize * nv);
-  L.ctrl = take(8 * d.nu);
-  L.alen = take(tsize * d.nu);
-  L.avel = take(tsize * d.nu);
-  L.aforce = take(tsize * d.nu);
-  L.bpos = take(tsize * 30 * A);
-  L.bR = take(tsize * 90 * A);
-  L.bcom = take(tsize * 30 * A);
-  L.bIw = take(tsize * 60 * A);
-  L.bF = take(tsize * 30 * A);
-  L.bN = take(tsize * 30 * A);
-  L.dax = take(tsize * 27 * A);
-  L.danc = take(tsize * 27 * A);
-  L.site = take(tsize * 3 * A);
-  L.cR = take(tsize * 9 * K);
-  L.Marm = take(tsize * 81 * A);
-  L.Larm = take(tsize * 81 * A);
-  L.LBarm = take(tsize * 81 * A);
-  L.gx = take(tsize * 4 * d.ngc);
-  L.ginfo = take(4 * d.ngc);
-  L.cbi = take(4 * 4 * d.ncb);
-  L.cbw = take(tsize * 8 * d.ncb);
-  L.cbg = take(2 * d.ngc);
-  L.sp = take(4 * WAVE);
-  L.spoff = take(4 * WAVE);
-  L.gsurv = take(4 * 2 * WAVE);
-  L.stage = take(tsize * 8 * d.maxcon);
-  L.skey = take(4 * d.maxcon);
-  L.spw = take(4 * d.maxcon);
-  L.cube = take(tsize * 4 * d.K);
-  L.H = take(tsize * nv * nv);
-  L.c_i = take(4 * 4 * d.maxcon);
-  L.c_r = take(tsize * CR_N * d.maxcon);
-  L.r_i = take(4 * 4 * d.maxrow);
-  L.r_r = take(tsize * RR_N * d.maxrow);
-  L.tmask = take(8 * d.ntree);
-  L.misc = take(4 * 16);
-  L.sort = take(4 * K);
-  L.uctl = take(8 * d.nu);
-  L.scal = take(8 * 4);
-  L.prof = take(8 * 16);
-  L.total = off;
-  return L;
+  return make_layout(d.A, d.K, d.nq, d.nv, d.nu, d.ngc, d.ncb, d.maxcon, d.maxrow, d.ntree, tsize);
 }
 
 template <typename T>
@@ -2602,6 +3026,8 @@ static Model<T> make_model(const fm_handle* h) {
   M.meaninertia = (const T*)h->meaninertia;
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
+  const char* cl = getenv("FM_CHOL_LDS");
+  M.dbg_flags = (cl && cl[0] == '1') ? 1 : 0;
   return M;
 }
 
@@ -2721,8 +3147,28 @@ static int create_typed(fm_handle* h) {
   HIPCHK(hipMemset(h->counters, 0, N * 4 * sizeof(int64_t)));
   h->lay = lds_layout(d, sizeof(T));
   if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
-  HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
-  HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
+  HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             h->lay.total));
+  // env-step kernel: a compile-time specialisation when the scene is one of FM_FIXED_SCENES
+  h->fixed = -1;
+  const char* force_dyn = getenv("FM_FORCE_DYNAMIC");
+  int idx = 0;
+#define X(a, k)                                                                                          \
+  if (h->fixed < 0 && !(force_dyn && force_dyn[0] == '1') && FixedDims<a, k>::matches(d)) {             \
+    h->fixed = idx;                                                                                      \
+    h->lay_step = FixedDims<a, k>::template layout<sizeof(T)>();                                         \
+    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<a, k>>,                             \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, h->lay_step.total));          \
+  }                                                                                                      \
+  idx++;
+  FM_FIXED_SCENES
+#undef X
+  (void)idx;
+  if (h->fixed < 0) {
+    h->lay_step = h->lay;
+    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               h->lay.total));
+  }
   return 0;
 }
 
@@ -2785,6 +3231,25 @@ static int set_state_typed(fm_handle* h, const char* src) {
   HIPCHK(hipMemcpy(h->rng, rg.data(), rg.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   h->was_reset = true;
   return FM_OK;
+}
+
+template <typename T>
+static void launch_step(fm_handle* h, const StepIO& io) {
+  const StepParams<T> pd{make_model<T>(h), make_state<T>(h), h->lay, io};
+  dim3 grid(h->dm.N), block(WAVE);
+  int idx = 0;
+#define X(a, k)                                                                                        \
+  if (h->fixed == idx) {                                                                               \
+    StepParams<T> pf = pd;                                                                             \
+    pf.L = h->lay_step;                                                                                \
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<a, k>>), grid, block, h->lay_step.total, h->stream, pf); \
+    return;                                                                                            \
+  }                                                                                                    \
+  idx++;
+  FM_FIXED_SCENES
+#undef X
+  (void)idx;
+  hipLaunchKernelGGL((step_kernel<T, Dims>), grid, block, h->lay.total, h->stream, pd);
 }
 
 extern "C" {
@@ -2903,16 +3368,17 @@ int fm_num_arenas(const fm_handle* h) { return h ? h->dm.N : -1; }
 int fm_nq(const fm_handle* h) { return h ? h->dm.nq : -1; }
 int fm_nv(const fm_handle* h) { return h ? h->dm.nv : -1; }
 int fm_nu(const fm_handle* h) { return h ? h->dm.nu : -1; }
+int fm_workspace_bytes(const fm_handle* h) { return h ? h->lay_step.total : -1; }
 
 int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
   dim3 grid(h->dm.N), block(WAVE);
   if (h->fp64) {
-    hipLaunchKernelGGL(reset_kernel<double>, grid, block, h->lay.total, h->stream, make_model<double>(h),
+    hipLaunchKernelGGL((reset_kernel<double, Dims>), grid, block, h->lay.total, h->stream, make_model<double>(h),
                        make_state<double>(h), h->lay, obs, mask);
   } else {
-    hipLaunchKernelGGL(reset_kernel<float>, grid, block, h->lay.total, h->stream, make_model<float>(h),
+    hipLaunchKernelGGL((reset_kernel<float, Dims>), grid, block, h->lay.total, h->stream, make_model<float>(h),
                        make_state<float>(h), h->lay, obs, mask);
   }
   HIPCHK(hipGetLastError());
@@ -2945,14 +3411,10 @@ int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8
     io.ep_len = info->episode_length;
     io.terminal_scores = info->terminal_scores;
   }
-  dim3 grid(h->dm.N), block(WAVE);
-  if (h->fp64) {
-    hipLaunchKernelGGL(step_kernel<double>, grid, block, h->lay.total, h->stream, make_model<double>(h),
-                       make_state<double>(h), h->lay, io);
-  } else {
-    hipLaunchKernelGGL(step_kernel<float>, grid, block, h->lay.total, h->stream, make_model<float>(h),
-                       make_state<float>(h), h->lay, io);
-  }
+  if (h->fp64)
+    launch_step<double>(h, io);
+  else
+    launch_step<float>(h, io);
   HIPCHK(hipGetLastError());
   return FM_OK;
 }
@@ -2982,14 +3444,14 @@ int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int c
   HIPCHK(hipMalloc(&dbuf, need * sizeof(double)));
   HIPCHK(hipMemset(dbuf, 0, need * sizeof(double)));
   if (h->fp64) {
-    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                h->lay.total));
-    hipLaunchKernelGGL(debug_kernel<double>, dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<double>(h),
+    hipLaunchKernelGGL((debug_kernel<double, Dims>), dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<double>(h),
                        make_state<double>(h), h->lay, arena, actuated, dbuf);
   } else {
-    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<float, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                h->lay.total));
-    hipLaunchKernelGGL(debug_kernel<float>, dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<float>(h),
+    hipLaunchKernelGGL((debug_kernel<float, Dims>), dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<float>(h),
                        make_state<float>(h), h->lay, arena, actuated, dbuf);
   }
   HIPCHK(hipGetLastError());
@@ -3033,3 +3495,18 @@ int fm_get_counters(fm_handle* h, int64_t* host_out) {
 }
 
 }  // extern "C"
+#ifdef FM_EXP_CHOLTEST
+namespace fm {
+__global__ void __launch_bounds__(64) chol_test_kernel(float* Hg, int nv, float* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* H = (float*)smem;
+  float* g = H + 64 * 64;
+  float* dir = g + 64;
+  for (int i = LANE; i < nv * nv; i += WAVE) H[i] = Hg[blockIdx.x * nv * nv + i];
+  if (LANE < nv) g[LANE] = Hg[LANE];
+  SYNC();
+  chol_solve_reg<float, 48>(H, H + 4096, nv, g, dir);
+  if (LANE < nv) out[blockIdx.x * 64 + LANE] = dir[LANE];
+}
+}
+#endif

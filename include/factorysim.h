@@ -103,6 +103,7 @@ int fm_num_arenas(const fm_handle* h);
 int fm_nq(const fm_handle* h);
 int fm_nv(const fm_handle* h);
 int fm_nu(const fm_handle* h);
+int fm_workspace_bytes(const fm_handle* h); /* LDS bytes of one arena's env-step workspace */
 
 /* reset(): reset arenas where mask[i] != 0 (device uint8 [N]; NULL = all) and write their obs.
  * Mirrors BaseEnv.reset_sim + FactoryManipulationEnv.reset (environments.py:204-248): the

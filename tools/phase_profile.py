@@ -42,6 +42,7 @@ def main():
     rep = {k: {"share": round(v / tot, 4), "us_per_arena_substep": round(v / sub * 1e6, 3)} for k, v in ph.items()}
     rep["_total_us_per_arena_substep"] = round(tot / sub * 1e6, 3)
     rep["_mean_ncon"] = round(ncon / sub, 3)
+    rep["_lds_bytes_per_arena"] = env._L.fm_workspace_bytes(env._h)
     rep["_newton_iters_per_substep"] = round(float(c1[1] - c0[1]) / sub, 3)
     print(json.dumps(rep, indent=1))
 
