@@ -32,6 +32,23 @@ def algorithmic_bytes(A, K):
     return 100 * 8 * (nq + 2 * nv + nu) + 4 * (act_dim + obs_dim + 4)
 
 
+def max_over_ranks(x, device=None):
+    """max of a host float over all ranks (the slowest rank's clock sets the job time); identity at N=1"""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device if device is not None else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_throughput(arenas_per_rank, steps, world, wall_max):
+    """whole-job env-steps/s: every rank steps its own arenas (weak scaling, no data-path collective)"""
+    return world * arenas_per_rank * steps / wall_max
+
+
 def cpu_baseline(A, K, seconds):
     """oracle env-steps/s on the host cores (OpenMP), bounded sample"""
     import ctypes as C
@@ -113,11 +130,8 @@ def main():
     t1 = time.perf_counter()
     wall = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # average step_kernel launch (only kernel in the region)
-    if world > 1:
-        tt = torch.tensor([wall], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        wall = tt.item()
-    value = world * N * args.steps / wall
+    wall = max_over_ranks(wall, device)
+    value = job_throughput(N, args.steps, world, wall)
     ctr = env.counters()
     dropped = int(ctr[:, 0].sum())
     if rank == 0:

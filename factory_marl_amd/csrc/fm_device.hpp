@@ -1,4 +1,5 @@
-// fm_kernel.hip -- the MI355X env-step pipeline: one workgroup (= one 64-lane wavefront) per arena.
+// fm_device.hpp -- the MI355X env-step pipeline (device code; kernels instantiated by fm_api.hip for
+// runtime dims and by fm_fixed.hip once per compile-time scene): one workgroup (= one 64-lane wavefront) per arena.
 //
 // One launch advances every arena by one env-step of the reference
 // (FactoryManipulationEnv.step -> BaseEnv.step_sim, environments.py:151-202, base_env.py:240-282):
@@ -16,6 +17,7 @@
 // Lane mapping: sequential chains run on few lanes (one lane per arm for FK + RNE, lane 0 for the task
 // layer); everything with natural width runs across the wave (geoms, broadphase pairs, narrowphase,
 // contact rows, Hessian entries, Cholesky trailing updates, line-search reductions).
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -32,10 +34,6 @@
 
 #ifndef FM_WS_RUNTIME_LAYOUT
 #define FM_WS_RUNTIME_LAYOUT 0
-#endif
-// scenes with a compile-time specialised env-step kernel: X(num_arms, max_num_objects)
-#ifndef FM_FIXED_SCENES
-#define FM_FIXED_SCENES X(2, 4) X(2, 8) X(2, 10)
 #endif
 
 namespace fm {
@@ -2897,616 +2895,3 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
 
 }  // namespace fm
 
-// =================================================================================================
-// host side: handle, uploads, C ABI
-// =================================================================================================
-using namespace fm;
-
-static thread_local std::string g_err;
-
-static int set_err(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-
-#define HIPCHK(x)                                                                                  \
-  do {                                                                                             \
-    hipError_t e_ = (x);                                                                           \
-    if (e_ != hipSuccess) return set_err(FM_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-struct fm_handle {
-  fm_config cfg;
-  SceneHost sc;
-  Dims dm;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  bool fp64 = false;
-  bool was_reset = false;
-  Lay lay;
-  std::vector<void*> allocs;
-  // device model arrays (typed by precision, stored as void*)
-  void* arm_base = nullptr;
-  void* body = nullptr;
-  void* dof = nullptr;
-  void* ctrlrange = nullptr;
-  void* geom = nullptr;
-  int* geom_i = nullptr;
-  int* ginfo = nullptr;
-  int* cbi = nullptr;
-  void* cbs = nullptr;
-  uint16_t* cbg = nullptr;
-  uint32_t* cbp = nullptr;
-  uint32_t* pair = nullptr;
-  void* param = nullptr;
-  void* cube = nullptr;
-  void* meaninertia = nullptr;
-  uint32_t* tri = nullptr;
-  // state
-  void* phys = nullptr;
-  double* dbl = nullptr;
-  int32_t* ints = nullptr;
-  uint64_t* rng = nullptr;
-  int64_t* counters = nullptr;
-  unsigned long long* prof = nullptr;
-  bool prof_on = false;
-  int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
-  Lay lay_step{};  // workspace layout of the env-step kernel in use
-};
-
-template <typename T>
-static int upload(fm_handle* h, void** dst, const std::vector<double>& src) {
-  std::vector<T> tmp(src.size());
-  for (size_t i = 0; i < src.size(); i++) tmp[i] = (T)src[i];
-  size_t bytes = std::max<size_t>(tmp.size(), 1) * sizeof(T);
-  HIPCHK(hipMalloc(dst, bytes));
-  h->allocs.push_back(*dst);
-  if (!tmp.empty()) HIPCHK(hipMemcpy(*dst, tmp.data(), tmp.size() * sizeof(T), hipMemcpyHostToDevice));
-  return 0;
-}
-
-template <typename U>
-static int upload_raw(fm_handle* h, U** dst, const std::vector<U>& src) {
-  size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(U);
-  HIPCHK(hipMalloc((void**)dst, bytes));
-  h->allocs.push_back(*dst);
-  if (!src.empty()) HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(U), hipMemcpyHostToDevice));
-  return 0;
-}
-
-static Lay lds_layout(const Dims& d, int tsize) {
-  return make_layout(d.A, d.K, d.nq, d.nv, d.nu, d.ngc, d.ncb, d.maxcon, d.maxrow, d.ntree, tsize);
-}
-
-template <typename T>
-static Model<T> make_model(const fm_handle* h) {
-  Model<T> M;
-  M.dm = h->dm;
-  M.dt = T(0.001);
-  M.grav = T(9.81);
-  M.belt_mass = T(1000);
-  M.belt_kv = T(1e4);
-  M.belt_damp = T(5e-4);
-  M.belt_invw_t = T((1.0 / 1000.0) / 3.0);
-  const fm_config& c = h->cfg;
-  M.init_speed = c.initial_conveyor_speed;
-  M.accel = c.conveyor_acceleration;
-  M.pt_time = c.pt_time;
-  M.force_thr = c.force_contact_threshold;
-  M.spawn_freq0 = c.spawn_freq * h->dm.A;
-  M.spawn_inc = c.spawn_freq_increase;
-  M.w_grip = c.gripper_to_closest_cube_reward_factor;
-  M.w_bucket = c.closest_cube_to_bucket_reward_factor;
-  M.w_action = c.small_action_norm_reward_factor;
-  M.base_reward = c.base_reward;
-  M.bucket_x0 = h->sc.bucket_x[0];
-  M.bucket_x1 = h->sc.bucket_x[1];
-  M.bucket_y = h->sc.bucket_y;
-  M.bucket_z = h->sc.bucket_z;
-  M.env_class = c.env_class;
-  M.solver_iter = c.solver_iterations;
-  M.solver_tol = c.solver_tolerance;
-  M.arm_base = (const T*)h->arm_base;
-  M.body = (const T*)h->body;
-  M.dof = (const T*)h->dof;
-  M.ctrlrange = (const T*)h->ctrlrange;
-  M.geom = (const T*)h->geom;
-  M.geom_i = h->geom_i;
-  M.pair = h->pair;
-  M.ginfo = h->ginfo;
-  M.cbi = h->cbi;
-  M.cbs = (const T*)h->cbs;
-  M.cbg = h->cbg;
-  M.cbp = h->cbp;
-  for (int a = 0; a < 5; a++)
-    for (int b = 0; b < 5; b++) M.ptab[5 * a + b] = h->sc.ptab[a][b];
-  M.param = (const T*)h->param;
-  M.cube = (const T*)h->cube;
-  M.meaninertia = (const T*)h->meaninertia;
-  M.tri = h->tri;
-  M.prof = h->prof_on ? h->prof : nullptr;
-  const char* cl = getenv("FM_CHOL_LDS");
-  M.dbg_flags = (cl && cl[0] == '1') ? 1 : 0;
-  return M;
-}
-
-template <typename T>
-static State<T> make_state(const fm_handle* h) {
-  State<T> S;
-  S.phys = (T*)h->phys;
-  S.dbl = h->dbl;
-  S.ints = h->ints;
-  S.rng = h->rng;
-  S.counters = h->counters;
-  return S;
-}
-
-template <typename T>
-static int create_typed(fm_handle* h) {
-  const SceneHost& s = h->sc;
-  const Dims& d = h->dm;
-  std::vector<double> arm_base(12 * s.A), body(32 * ARM_NB, 0.0), dof(4 * ARM_ND, 0.0), ctrl(2 * s.nu);
-  for (int i = 0; i < s.A; i++)
-    for (int k = 0; k < 12; k++) arm_base[12 * i + k] = s.arm_base[i][k];
-  for (int b = 0; b < ARM_NB; b++) {
-    double* o = &body[32 * b];
-    for (int k = 0; k < 12; k++) o[k] = s.body_local[b][k];
-    o[12] = s.body_mass[b];
-    for (int k = 0; k < 3; k++) o[13 + k] = s.body_ipos[b][k];
-    for (int k = 0; k < 9; k++) o[16 + k] = s.body_iR[b][k];
-    for (int k = 0; k < 3; k++) o[25 + k] = s.body_I[b][k];
-    o[28] = s.body_invw[b][0];
-    o[29] = s.body_invw[b][1];
-  }
-  for (int j = 0; j < ARM_ND; j++) {
-    dof[4 * j] = s.dof_range[j][0];
-    dof[4 * j + 1] = s.dof_range[j][1];
-    dof[4 * j + 2] = s.dof_invw[j];
-  }
-  for (int u = 0; u < s.nu; u++) {
-    ctrl[2 * u] = s.ctrlrange[u][0];
-    ctrl[2 * u + 1] = s.ctrlrange[u][1];
-  }
-  int ngc = (int)s.geoms.size();
-  std::vector<double> geom(16 * ngc, 0.0), param(8 * s.params.size(), 0.0);
-  std::vector<int> geom_i(4 * ngc);
-  for (int g = 0; g < ngc; g++) {
-    const GeomRec& r = s.geoms[g];
-    for (int k = 0; k < 3; k++) geom[16 * g + k] = r.pos[k];
-    for (int k = 0; k < 9; k++) geom[16 * g + 3 + k] = r.R[k];
-    for (int k = 0; k < 3; k++) geom[16 * g + 12 + k] = r.size[k];
-    geom[16 * g + 15] = r.rbound;
-    geom_i[4 * g] = r.mjid;
-    geom_i[4 * g + 1] = r.type;
-    geom_i[4 * g + 2] = r.kbody;
-    geom_i[4 * g + 3] = s.box_slot[g];
-  }
-  // cube bounding radius depends on the per-arena size: use the largest possible (h <= 0.05)
-  for (int g = 0; g < ngc; g++)
-    if (s.geoms[g].kbody >= 2 && s.geoms[g].kbody < 2 + s.K) geom[16 * g + 15] = std::sqrt(3.0) * 0.05;
-  for (size_t p = 0; p < s.params.size(); p++) {
-    param[8 * p] = s.params[p].mu;
-    param[8 * p + 1] = s.params[p].solref[0];
-    param[8 * p + 2] = s.params[p].solref[1];
-    for (int k = 0; k < 5; k++) param[8 * p + 3 + k] = s.params[p].solimp[k];
-  }
-  int r;
-  if ((r = upload<T>(h, &h->arm_base, arm_base))) return r;
-  if ((r = upload<T>(h, &h->body, body))) return r;
-  if ((r = upload<T>(h, &h->dof, dof))) return r;
-  if ((r = upload<T>(h, &h->ctrlrange, ctrl))) return r;
-  if ((r = upload<T>(h, &h->geom, geom))) return r;
-  if ((r = upload_raw<int>(h, &h->geom_i, geom_i))) return r;
-  if ((r = upload_raw<uint32_t>(h, &h->pair, s.pairs))) return r;
-  {
-    std::vector<int> gin(ngc), cbi(4 * s.cbodies.size());
-    std::vector<double> cbs(8 * s.cbodies.size(), 0.0);
-    for (int g = 0; g < ngc; g++) {
-      const GeomRec& G = s.geoms[g];
-      int tc = G.type == GT_PLANE ? GC_PLANE : (G.type == GT_SPHERE ? GC_SPHERE : GC_BOX);
-      int arm = G.mjid >= 13 + s.K ? 1 : 0;
-      gin[g] = tc | (arm << GI_ARM) | (G.pclass << GI_PC) | (G.kbody << 8);
-    }
-    for (size_t b = 0; b < s.cbodies.size(); b++) {
-      const CBody& c = s.cbodies[b];
-      cbi[4 * b] = c.kbody;
-      cbi[4 * b + 1] = c.flags;
-      cbi[4 * b + 2] = c.g0;
-      cbi[4 * b + 3] = c.ng;
-      for (int k = 0; k < 3; k++) {
-        cbs[8 * b + k] = c.c[k];
-        cbs[8 * b + 4 + k] = c.e[k];
-      }
-      cbs[8 * b + 3] = c.r;
-    }
-    if ((r = upload_raw<int>(h, &h->ginfo, gin))) return r;
-    if ((r = upload_raw<int>(h, &h->cbi, cbi))) return r;
-    if ((r = upload<T>(h, &h->cbs, cbs))) return r;
-    if ((r = upload_raw<uint16_t>(h, &h->cbg, s.cb_geoms))) return r;
-    if ((r = upload_raw<uint32_t>(h, &h->cbp, s.cb_pairs))) return r;
-  }
-  if ((r = upload<T>(h, &h->param, param))) return r;
-  if ((r = upload<T>(h, &h->cube, s.cube))) return r;
-  if ((r = upload<T>(h, &h->meaninertia, s.meaninertia))) return r;
-  if ((r = upload_raw<uint32_t>(h, &h->tri, s.tri))) return r;
-  // state
-  size_t N = d.N;
-  HIPCHK(hipMalloc(&h->phys, N * d.phys_stride * sizeof(T)));
-  h->allocs.push_back(h->phys);
-  HIPCHK(hipMemset(h->phys, 0, N * d.phys_stride * sizeof(T)));
-  HIPCHK(hipMalloc((void**)&h->dbl, N * d.dbl_stride * sizeof(double)));
-  h->allocs.push_back(h->dbl);
-  HIPCHK(hipMemset(h->dbl, 0, N * d.dbl_stride * sizeof(double)));
-  HIPCHK(hipMalloc((void**)&h->ints, N * d.int_stride * sizeof(int32_t)));
-  h->allocs.push_back(h->ints);
-  HIPCHK(hipMemset(h->ints, 0, N * d.int_stride * sizeof(int32_t)));
-  if ((r = upload_raw<uint64_t>(h, &h->rng, s.rng_init))) return r;
-  HIPCHK(hipMalloc((void**)&h->counters, N * 4 * sizeof(int64_t)));
-  h->allocs.push_back(h->counters);
-  HIPCHK(hipMemset(h->counters, 0, N * 4 * sizeof(int64_t)));
-  h->lay = lds_layout(d, sizeof(T));
-  if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
-  HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             h->lay.total));
-  // env-step kernel: a compile-time specialisation when the scene is one of FM_FIXED_SCENES
-  h->fixed = -1;
-  const char* force_dyn = getenv("FM_FORCE_DYNAMIC");
-  int idx = 0;
-#define X(a, k)                                                                                          \
-  if (h->fixed < 0 && !(force_dyn && force_dyn[0] == '1') && FixedDims<a, k>::matches(d)) {             \
-    h->fixed = idx;                                                                                      \
-    h->lay_step = FixedDims<a, k>::template layout<sizeof(T)>();                                         \
-    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<a, k>>,                             \
-                               hipFuncAttributeMaxDynamicSharedMemorySize, h->lay_step.total));          \
-  }                                                                                                      \
-  idx++;
-  FM_FIXED_SCENES
-#undef X
-  (void)idx;
-  if (h->fixed < 0) {
-    h->lay_step = h->lay;
-    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               h->lay.total));
-  }
-  return 0;
-}
-
-static int state_record_size(const fm_handle* h) {
-  return (int)((h->dm.phys_stride + h->dm.dbl_stride) * sizeof(double) + h->dm.int_stride * sizeof(int32_t) +
-               4 * sizeof(uint64_t));
-}
-
-template <typename T>
-static int get_state_typed(fm_handle* h, char* out) {
-  const Dims& d = h->dm;
-  size_t N = d.N;
-  std::vector<T> ph(N * d.phys_stride);
-  std::vector<double> db(N * d.dbl_stride);
-  std::vector<int32_t> in(N * d.int_stride);
-  std::vector<uint64_t> rg(N * 4);
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(ph.data(), h->phys, ph.size() * sizeof(T), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(db.data(), h->dbl, db.size() * sizeof(double), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(in.data(), h->ints, in.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(rg.data(), h->rng, rg.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  size_t rec = state_record_size(h);
-  for (size_t n = 0; n < N; n++) {
-    char* o = out + n * rec;
-    double* dp = (double*)o;
-    for (int i = 0; i < d.phys_stride; i++) dp[i] = (double)ph[n * d.phys_stride + i];
-    for (int i = 0; i < d.dbl_stride; i++) dp[d.phys_stride + i] = db[n * d.dbl_stride + i];
-    int32_t* ip = (int32_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double));
-    for (int i = 0; i < d.int_stride; i++) ip[i] = in[n * d.int_stride + i];
-    uint64_t* up = (uint64_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double) + d.int_stride * sizeof(int32_t));
-    for (int i = 0; i < 4; i++) up[i] = rg[n * 4 + i];
-  }
-  return FM_OK;
-}
-
-template <typename T>
-static int set_state_typed(fm_handle* h, const char* src) {
-  const Dims& d = h->dm;
-  size_t N = d.N;
-  std::vector<T> ph(N * d.phys_stride);
-  std::vector<double> db(N * d.dbl_stride);
-  std::vector<int32_t> in(N * d.int_stride);
-  std::vector<uint64_t> rg(N * 4);
-  size_t rec = state_record_size(h);
-  for (size_t n = 0; n < N; n++) {
-    const char* o = src + n * rec;
-    const double* dp = (const double*)o;
-    for (int i = 0; i < d.phys_stride; i++) ph[n * d.phys_stride + i] = (T)dp[i];
-    for (int i = 0; i < d.dbl_stride; i++) db[n * d.dbl_stride + i] = dp[d.phys_stride + i];
-    const int32_t* ip = (const int32_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double));
-    for (int i = 0; i < d.int_stride; i++) in[n * d.int_stride + i] = ip[i];
-    const uint64_t* up =
-        (const uint64_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double) + d.int_stride * sizeof(int32_t));
-    for (int i = 0; i < 4; i++) rg[n * 4 + i] = up[i];
-  }
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(h->phys, ph.data(), ph.size() * sizeof(T), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->rng, rg.data(), rg.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-  h->was_reset = true;
-  return FM_OK;
-}
-
-template <typename T>
-static void launch_step(fm_handle* h, const StepIO& io) {
-  const StepParams<T> pd{make_model<T>(h), make_state<T>(h), h->lay, io};
-  dim3 grid(h->dm.N), block(WAVE);
-  int idx = 0;
-#define X(a, k)                                                                                        \
-  if (h->fixed == idx) {                                                                               \
-    StepParams<T> pf = pd;                                                                             \
-    pf.L = h->lay_step;                                                                                \
-    hipLaunchKernelGGL((step_kernel<T, FixedDims<a, k>>), grid, block, h->lay_step.total, h->stream, pf); \
-    return;                                                                                            \
-  }                                                                                                    \
-  idx++;
-  FM_FIXED_SCENES
-#undef X
-  (void)idx;
-  hipLaunchKernelGGL((step_kernel<T, Dims>), grid, block, h->lay.total, h->stream, pd);
-}
-
-extern "C" {
-
-void fm_config_default(fm_config* c) {
-  std::memset(c, 0, sizeof *c);
-  c->num_arenas = 1;
-  c->num_arms = 2;
-  c->max_num_objects = 10;
-  c->env_class = FM_ENV_ALLFULLRL_PROGRESS;
-  c->precision = FM_FP32;
-  c->max_contacts = 0;
-  c->initial_conveyor_speed = 0.1;
-  c->conveyor_acceleration = 0.001;
-  c->pt_time = 0.2;
-  c->force_contact_threshold = 200.0;
-  c->control_frequency = 10;
-  c->spawn_freq = 1.0 / 10;
-  c->spawn_freq_increase = 1.001;
-  c->gripper_to_closest_cube_reward_factor = 0.2;
-  c->closest_cube_to_bucket_reward_factor = 0.4;
-  c->small_action_norm_reward_factor = 0.0;
-  c->base_reward = 0.4;
-  c->solver_iterations = 100;
-  c->solver_tolerance = 0.0;  // 0 = precision default (see fm_create)
-}
-
-const char* fm_last_error(void) { return g_err.c_str(); }
-
-int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle** out) {
-  if (!cfg || !out) return set_err(FM_EINVAL, "null argument");
-  *out = nullptr;
-  fm_handle* h = new fm_handle();
-  h->cfg = *cfg;
-  h->device = device;
-  h->fp64 = cfg->precision == FM_FP64;
-  if (cfg->env_class != FM_ENV_FACTORY_SCORE && cfg->env_class != FM_ENV_ALLFULLRL_PROGRESS) {
-    delete h;
-    return set_err(FM_EINVAL, "unknown env_class");
-  }
-  if (h->cfg.solver_tolerance <= 0) h->cfg.solver_tolerance = h->fp64 ? 1e-12 : 1e-7;
-  if (h->cfg.solver_iterations <= 0) h->cfg.solver_iterations = 100;
-  std::string err;
-  if (!build_scene(cfg->num_arms, cfg->max_num_objects, cfg->num_arenas, seeds, h->sc, err)) {
-    delete h;
-    return set_err(FM_EINVAL, err);
-  }
-  const SceneHost& s = h->sc;
-  Dims& d = h->dm;
-  d.N = s.N;
-  d.A = s.A;
-  d.K = s.K;
-  d.nq = s.nq;
-  d.nv = s.nv;
-  d.nu = s.nu;
-  d.ngc = (int)s.geoms.size();
-  d.nbox = s.nbox;
-  d.npair = (int)s.pairs.size();
-  d.nparam = (int)s.params.size();
-  d.ntree = 1 + s.K + s.A;
-  d.ncb = (int)s.cbodies.size();
-  d.ncbp = (int)s.cb_pairs.size();
-  d.obs_dim = s.obs_dim;
-  d.act_dim = s.act_dim;
-  d.frame_skip = (int)((1.0 / cfg->control_frequency) / 0.001);
-  d.maxcon = cfg->max_contacts > 0 ? std::min(cfg->max_contacts, MAXCON) : MAXCON;
-  d.maxrow = 10 * s.A;
-  d.phys_stride = 2 * s.nq + 3 * s.nv;
-  d.dbl_stride = s.nu + 3 + 2 * s.A + 1;
-  d.int_stride = 2 * s.K + I_NINT;
-  if (hipSetDevice(device) != hipSuccess) {
-    delete h;
-    return set_err(FM_EDEVICE, "hipSetDevice failed");
-  }
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
-    return set_err(FM_EDEVICE, "hipStreamCreate failed");
-  }
-  h->own_stream = true;
-  int r = h->fp64 ? create_typed<double>(h) : create_typed<float>(h);
-  if (r) {
-    std::string e = g_err;
-    fm_destroy(h);
-    return set_err(r, e);
-  }
-  *out = h;
-  return FM_OK;
-}
-
-void fm_destroy(fm_handle* h) {
-  if (!h) return;
-  (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (void* p : h->allocs) (void)hipFree(p);
-  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
-  delete h;
-}
-
-int fm_set_stream(fm_handle* h, void* stream) {
-  if (!h) return set_err(FM_EINVAL, "null handle");
-  h->stream = (hipStream_t)stream;  // NULL = the legacy default stream (torch's default stream)
-  return FM_OK;
-}
-
-int fm_sync(fm_handle* h) {
-  if (!h) return set_err(FM_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipGetLastError());
-  return FM_OK;
-}
-
-int fm_obs_dim(const fm_handle* h) { return h ? h->dm.obs_dim : -1; }
-int fm_act_dim(const fm_handle* h) { return h ? h->dm.act_dim : -1; }
-int fm_num_arenas(const fm_handle* h) { return h ? h->dm.N : -1; }
-int fm_nq(const fm_handle* h) { return h ? h->dm.nq : -1; }
-int fm_nv(const fm_handle* h) { return h ? h->dm.nv : -1; }
-int fm_nu(const fm_handle* h) { return h ? h->dm.nu : -1; }
-int fm_workspace_bytes(const fm_handle* h) { return h ? h->lay_step.total : -1; }
-
-int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
-  if (!h) return set_err(FM_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(h->device));
-  dim3 grid(h->dm.N), block(WAVE);
-  if (h->fp64) {
-    hipLaunchKernelGGL((reset_kernel<double, Dims>), grid, block, h->lay.total, h->stream, make_model<double>(h),
-                       make_state<double>(h), h->lay, obs, mask);
-  } else {
-    hipLaunchKernelGGL((reset_kernel<float, Dims>), grid, block, h->lay.total, h->stream, make_model<float>(h),
-                       make_state<float>(h), h->lay, obs, mask);
-  }
-  HIPCHK(hipGetLastError());
-  h->was_reset = true;
-  return FM_OK;
-}
-
-int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
-            const fm_info* info) {
-  if (!h) return set_err(FM_EINVAL, "null handle");
-  if (!actions) return set_err(FM_EINVAL, "actions is NULL");
-  if (!h->was_reset) return set_err(FM_ESTATE, "fm_step before fm_reset");
-  HIPCHK(hipSetDevice(h->device));
-  StepIO io;
-  std::memset(&io, 0, sizeof io);
-  io.actions = actions;
-  io.obs = obs;
-  io.reward = reward;
-  io.terminated = terminated;
-  io.truncated = truncated;
-  if (info) {
-    io.scores = info->scores;
-    io.num_obj = info->num_obj;
-    io.play_time = info->play_time;
-    io.conveyor_speed = info->conveyor_speed;
-    io.out_of_reach = info->out_of_reach;
-    io.force_terminate = info->force_terminate;
-    io.terminal_obs = info->terminal_obs;
-    io.ep_return = info->episode_return;
-    io.ep_len = info->episode_length;
-    io.terminal_scores = info->terminal_scores;
-  }
-  if (h->fp64)
-    launch_step<double>(h, io);
-  else
-    launch_step<float>(h, io);
-  HIPCHK(hipGetLastError());
-  return FM_OK;
-}
-
-// exported record: doubles [phys (2nq+3nv) | dbl_stride] , int32 [int_stride], uint64 [4]
-int fm_state_size(const fm_handle* h) { return h ? state_record_size(h) : -1; }
-
-int fm_get_state(fm_handle* h, void* host_out) {
-  if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
-  return h->fp64 ? get_state_typed<double>(h, (char*)host_out) : get_state_typed<float>(h, (char*)host_out);
-}
-
-int fm_set_state(fm_handle* h, const void* host_in) {
-  if (!h || !host_in) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
-  return h->fp64 ? set_state_typed<double>(h, (const char*)host_in) : set_state_typed<float>(h, (const char*)host_in);
-}
-
-int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int cap) {
-  if (!h || !host_out || arena < 0 || arena >= h->dm.N) return set_err(FM_EINVAL, "bad argument");
-  const Dims& d = h->dm;
-  int need = 2 + 81 * d.A + 4 * d.nv + 3 * d.A + 60 * d.A + 27 * d.A + 17 * 64 + 6 * 20 * d.A;
-  if (cap < need) return set_err(FM_EINVAL, "buffer too small: need " + std::to_string(need));
-  HIPCHK(hipSetDevice(h->device));
-  double* dbuf = nullptr;
-  HIPCHK(hipMalloc(&dbuf, need * sizeof(double)));
-  HIPCHK(hipMemset(dbuf, 0, need * sizeof(double)));
-  if (h->fp64) {
-    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               h->lay.total));
-    hipLaunchKernelGGL((debug_kernel<double, Dims>), dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<double>(h),
-                       make_state<double>(h), h->lay, arena, actuated, dbuf);
-  } else {
-    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<float, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               h->lay.total));
-    hipLaunchKernelGGL((debug_kernel<float, Dims>), dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<float>(h),
-                       make_state<float>(h), h->lay, arena, actuated, dbuf);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(host_out, dbuf, need * sizeof(double), hipMemcpyDeviceToHost));
-  HIPCHK(hipFree(dbuf));
-  return need;
-}
-
-int fm_profile(fm_handle* h, int mode, uint64_t* host_out) {
-  if (!h) return set_err(FM_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(h->device));
-  if (!h->prof) {
-    HIPCHK(hipMalloc((void**)&h->prof, 16 * sizeof(unsigned long long)));
-    h->allocs.push_back(h->prof);
-    HIPCHK(hipMemset(h->prof, 0, 16 * sizeof(unsigned long long)));
-  }
-  if (host_out) {
-    HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemcpy(host_out, h->prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    int khz = 0;
-    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
-    host_out[15] = (uint64_t)khz;
-  }
-  if (mode == 1) {
-    HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemset(h->prof, 0, 16 * sizeof(unsigned long long)));
-    h->prof_on = true;
-  } else if (mode == 0) {
-    h->prof_on = false;
-  }
-  return FM_OK;
-}
-
-int fm_get_counters(fm_handle* h, int64_t* host_out) {
-  if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
-  return FM_OK;
-}
-
-}  // extern "C"
-#ifdef FM_EXP_CHOLTEST
-namespace fm {
-__global__ void __launch_bounds__(64) chol_test_kernel(float* Hg, int nv, float* out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* H = (float*)smem;
-  float* g = H + 64 * 64;
-  float* dir = g + 64;
-  for (int i = LANE; i < nv * nv; i += WAVE) H[i] = Hg[blockIdx.x * nv * nv + i];
-  if (LANE < nv) g[LANE] = Hg[LANE];
-  SYNC();
-  chol_solve_reg<float, 48>(H, H + 4096, nv, g, dir);
-  if (LANE < nv) out[blockIdx.x * 64 + LANE] = dir[LANE];
-}
-}
-#endif

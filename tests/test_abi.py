@@ -1,0 +1,105 @@
+"""The C-ABI boundary (include/factorysim.h) without a GPU: the HIP library loads, exports every function
+the header declares, the Python binding registers the same set, and the product path refuses to run
+without a device instead of falling back to the CPU."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "factorysim.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fm_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from factory_marl_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libfactorysim.so not built (run `python __graft_entry__.py`)")
+    return _lib.load()
+
+
+def test_header_declares_the_entry_points():
+    fns = header_functions()
+    for need in ["fm_create", "fm_destroy", "fm_reset", "fm_step", "fm_get_state", "fm_set_state", "fm_set_stream"]:
+        assert need in fns
+
+
+def test_library_exports_every_header_symbol(lib):
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_binding_registers_the_header_set():
+    from factory_marl_amd import _lib
+
+    assert sorted(_lib.EXPORTED) == header_functions()
+
+
+def test_config_defaults_match_the_reference(lib):
+    from factory_marl_amd import _lib
+
+    c = _lib.FmConfig()
+    lib.fm_config_default(C.byref(c))
+    # challenge_env/base_env.py defaults
+    assert c.num_arms == 2 and c.max_num_objects == 10
+    assert c.initial_conveyor_speed == pytest.approx(0.1)
+    assert c.conveyor_acceleration == pytest.approx(0.001)
+    assert c.pt_time == pytest.approx(0.2)
+    assert c.force_contact_threshold == pytest.approx(200.0)
+    assert c.control_frequency == pytest.approx(10.0)
+    assert c.spawn_freq_increase == pytest.approx(1.001)
+
+
+def test_create_fails_loudly_without_a_device(lib):
+    """no GPU here: fm_create must return an error (never a CPU fallback)"""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from factory_marl_amd import _lib
+
+    c = _lib.FmConfig()
+    lib.fm_config_default(C.byref(c))
+    c.num_arenas = 2
+    c.max_num_objects = 4
+    h = C.c_void_p()
+    rc = lib.fm_create(C.byref(c), 0, None, C.byref(h))
+    assert rc != 0
+    assert lib.fm_last_error().decode()
+
+
+def test_vec_env_raises_without_library(monkeypatch, tmp_path):
+    from factory_marl_amd import _lib
+
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_LIB", None)
+    with pytest.raises(_lib.FactorySimError):
+        _lib.load()
+
+
+def test_state_record_roundtrip():
+    from factory_marl_amd import state as st
+
+    A, K = 2, 4
+    nq, nv, nu, nd, ni = st.sizes(A, K)
+    rng = np.random.default_rng(0)
+    d = rng.normal(size=nd)
+    i = rng.integers(-5, 100, ni).astype(np.int32)
+    r = rng.integers(0, 2**63, 4, dtype=np.uint64)
+    rec = st.pack(A, K, d, i, r)
+    assert rec.nbytes == st.record_bytes(A, K)
+    d2, i2, r2 = st.unpack(A, K, rec)
+    assert np.array_equal(d, d2) and np.array_equal(i, i2) and np.array_equal(r, r2)
+    f = st.fields(A, K, d)
+    assert f["qpos"].shape == (nq,) and f["ctrl_target"].shape == (nu,) and f["episode_return"].shape == (1,)
+    # sizes of the benchmark scene (nq 47, nv 43, nu 17, obs 100)
+    assert (nq, nv, nu) == (47, 43, 17)
