@@ -134,6 +134,8 @@ def main():
     value = job_throughput(N, args.steps, world, wall)
     ctr = env.counters()
     dropped = int(ctr[:, 0].sum())
+    diag = {"contacts_dropped": dropped, "newton_iters_per_substep": round(float(ctr[:, 1].sum()) / (N * total * 100), 3),
+            "newton_maxiter_hits": int(ctr[:, 2].sum()), "arenas_with_maxiter": int((ctr[:, 2] > 0).sum())}
     if rank == 0:
         B = algorithmic_bytes(A, K)
         achieved = N * B / (kern_ms * 1e-3) / 1e9
@@ -166,7 +168,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                          "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
                          "algorithmic_bytes_per_arena_step": B},
-            "contacts_dropped": dropped,
+            "diagnostics": diag,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(A, K, args.cpu_seconds)

@@ -511,6 +511,9 @@ __device__ __forceinline__ int dof_tree(const DD& d, int i) {
 // ------------------------------------------------------------------------------------------------
 // impedance / reference acceleration parameters (MuJoCo getimpedance, getKBIP with refsafe)
 // ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void sincos_t(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ void sincos_t(double x, double* s, double* c) { sincos(x, s, c); }
+
 template <typename T>
 __device__ __forceinline__ T impedance(const T* si, T x) {
   T dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
@@ -524,6 +527,8 @@ __device__ __forceinline__ T impedance(const T* si, T x) {
   T y;
   if (power == T(1))
     y = x;
+  else if (power == T(2))  // every contact class of this scene (solimp power 2): pow without the library call
+    y = x <= mid ? x * x / mid : T(1) - (T(1) - x) * (T(1) - x) / (T(1) - mid);
   else if (x <= mid)
     y = pow(x, power) / pow(mid, power - T(1));
   else
@@ -1185,7 +1190,8 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
         dax[3 * b + k] = ax[k];
         danc[3 * b + k] = o[k];
       }
-      T c = cos(q[b]), s = sin(q[b]);
+      T s, c;
+      sincos_t(q[b], &s, &c);
       // R = Rpre * Rz(q)
       for (int r = 0; r < 3; r++) {
         R[3 * r + 0] = Rpre[3 * r + 0] * c + Rpre[3 * r + 1] * s;
@@ -2137,8 +2143,12 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SYNC();
     PMARK(PH_NLS);
     T improvement = scale * (cost - newcost);
+    // fp32: the cost itself carries rounding noise of a few ulp of its magnitude; an "improvement" inside
+    // that band is not progress (without this a stiff arena can spin to the iteration cap, and one such
+    // arena sets the whole launch's duration)
+    const T noise = sizeof(T) == 4 ? T(4.8e-7) * fabs(scale * newcost) : T(0);
     cost = newcost;
-    if (improvement < tol) {
+    if (improvement < tol || improvement <= noise) {
       it++;
       break;
     }
