@@ -128,7 +128,7 @@ struct Lay {
   int r_i;    // int [maxrow][4]
   int r_r;    // T [maxrow][8]
   int tmask;  // uint64 [ntree]
-  int misc;   // int [16]
+  int misc;   // int [16 + 64]
   int sort;   // int [K]
   int uctl;   // double [nu]  clipped control of this env-step
   int scal;   // double [4]   per-step scalars broadcast from lane 0
@@ -139,7 +139,8 @@ struct Lay {
 
 // per-contact real record
 enum { CR_DIST = 0, CR_MU, CR_D, CR_KD, CR_BD, CR_POS, CR_FR = CR_POS + 3, CR_J = CR_FR + 9, CR_VEL = CR_J + 3 * CJ,
-       CR_JA = CR_VEL + 3, CR_JD = CR_JA + 3, CR_F = CR_JD + 3, CR_N = CR_F + 4 };
+       CR_JA = CR_VEL + 3, CR_JD = CR_JA + 3, CR_F = CR_JD + 3, CR_N = CR_F + 4,
+       CR_K = CR_JD /* 6 slots over JD+F: K_c during the Hessian build only */ };
 // generic row record (equality / joint limit)
 enum { RR_C0 = 0, RR_C1, RR_POS, RR_D, RR_AREF, RR_JAR, RR_JD, RR_F, RR_N };
 // phase slots of the optional wall-clock profile (fm_profile)
@@ -287,7 +288,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.cbw = take(tsize * 8 * ncb);
   L.sp = take(4 * WAVE);
   L.spoff = take(4 * WAVE);
-  L.gsurv = take(4 * 2 * WAVE);
+  L.gsurv = take(4 * 4 * WAVE);
   L.stage = take(tsize * 8 * maxcon);
   L.skey = take(4 * maxcon);
   L.spw = take(4 * maxcon);
@@ -301,7 +302,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.r_i = take(4 * 4 * maxrow);
   L.r_r = take(tsize * RR_N * maxrow);
   L.tmask = take(8 * ntree);
-  L.misc = take(4 * 16);
+  L.misc = take(4 * (16 + WAVE));  // 16 scalars + the Hessian assembly's block offsets
   L.sort = take(4 * K);
   L.uctl = take(8 * nu);
   L.scal = take(8 * 4);

@@ -39,7 +39,12 @@
 namespace fm {
 
 #define LANE ((int)threadIdx.x)
-#define SYNC() __syncthreads()
+// A workgroup is exactly one wave, and a wave's LDS instructions execute in issue order, so LDS
+// hand-offs between lanes need only a compiler barrier (no s_barrier, no waitcnt-draining fences).
+// FULL_SYNC() (a real workgroup barrier with memory fences) is kept where lanes hand data to each
+// other through GLOBAL memory: the lane-0 task layer's records read back by the observation writer.
+#define SYNC() asm volatile("" ::: "memory")
+#define FULL_SYNC() __syncthreads()
 
 template <typename T, typename DIM>
 struct Ws {
@@ -1013,8 +1018,12 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   SYNC();
   uint32_t* sp = w.sp();
   int* spoff = w.spoff();
+  // survivors are binned by narrowphase cost: box-box pairs (SAT + face clipping) in gsb, everything else
+  // (sphere-box, sphere-sphere, plane-*) in gs, so a batch of 64 lanes runs one code path instead of the
+  // union of all of them
   uint32_t* gs = w.gsurv();
-  int nsurv = 0;
+  uint32_t* gsb = gs + 2 * WAVE;
+  int nsurv = 0, nbb = 0;
   for (int p0 = 0; p0 < dm.ncbp; p0 += WAVE) {
     const int pidx = p0 + LANE;
     bool hit = false;
@@ -1095,9 +1104,13 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
           pk = (uint32_t)c1 | ((uint32_t)c2 << 12) | ((uint32_t)M.ptab[pc] << 24);
         }
       }
-      const uint64_t b2m = __ballot(ok);
-      if (ok) gs[nsurv + __popcll(b2m & below)] = pk;
+      const bool isbb = ok && (gin[pk & 4095] & 3) == GC_BOX;  // type-ordered: c1 box => both boxes
+      const uint64_t b2m = __ballot(ok && !isbb);
+      const uint64_t bbm = __ballot(isbb);
+      if (ok && !isbb) gs[nsurv + __popcll(b2m & below)] = pk;
+      if (isbb) gsb[nbb + __popcll(bbm & below)] = pk;
       nsurv += __popcll(b2m);
+      nbb += __popcll(bbm);
       SYNC();
       if (nsurv >= WAVE) {
         narrow_batch(M, w, gs, WAVE);
@@ -1108,10 +1121,20 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
         nsurv -= WAVE;
         SYNC();
       }
+      if (nbb >= WAVE) {
+        narrow_batch(M, w, gsb, WAVE);
+        const bool mv = LANE + WAVE < nbb;
+        uint32_t t = mv ? gsb[LANE + WAVE] : 0u;
+        SYNC();
+        if (mv) gsb[LANE] = t;
+        nbb -= WAVE;
+        SYNC();
+      }
     }
     SYNC();
   }
   if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
+  if (nbb > 0) narrow_batch(M, w, gsb, nbb);
   SYNC();
   // 5. sort the staged contacts by key into the contact slots
   const int nst = misc[MISC_NSTAGE];
@@ -1943,42 +1966,74 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       }
     }
     SYNC();
-    for (int c = 0; c < ncon; c++) {
-      const int* ci = w.ci() + 4 * c;
-      const T* cr = w.cr() + CR_N * c;
-      T mu = cr[CR_MU], D = cr[CR_D];
-      T Kc[6] = {0, 0, 0, 0, 0, 0};  // 00 11 22 01 02 12
-      bool any = false;
-      for (int e = 0; e < 4; e++) {
-        T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
-        T jar = edge_val(cr + CR_JA, mu, e) - aref;
-        if (jar < T(0)) {
-          any = true;
-          T sg = (e & 1) ? -mu : mu;
-          Kc[0] += D;
-          if (e < 2) {
-            Kc[1] += D * sg * sg;
-            Kc[3] += D * sg;
-          } else {
-            Kc[2] += D * sg * sg;
-            Kc[4] += D * sg;
+    // contact blocks B_c' K_c B_c: K_c (3x3, from the active pyramid edges) for every contact at once, then
+    // all (contact, block entry) pairs in one pass accumulated with LDS atomics (one wave: deterministic)
+    {
+      int sz = 0;
+      if (LANE < ncon) {
+        T* cr = w.cr() + CR_N * LANE;
+        const int* ci = w.ci() + 4 * LANE;
+        T mu = cr[CR_MU], D = cr[CR_D];
+        T Kc[6] = {0, 0, 0, 0, 0, 0};  // 00 11 22 01 02 12
+        bool any = false;
+        for (int e = 0; e < 4; e++) {
+          T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+          T jar = edge_val(cr + CR_JA, mu, e) - aref;
+          if (jar < T(0)) {
+            any = true;
+            T sg = (e & 1) ? -mu : mu;
+            Kc[0] += D;
+            if (e < 2) {
+              Kc[1] += D * sg * sg;
+              Kc[3] += D * sg;
+            } else {
+              Kc[2] += D * sg * sg;
+              Kc[4] += D * sg;
+            }
           }
         }
+        for (int k = 0; k < 6; k++) cr[CR_K + k] = Kc[k];
+        const int ncol = ((ci[3] >> 20) & 15) + ((ci[3] >> 24) & 15);
+        sz = any ? ncol * ncol : 0;
       }
-      if (!any) continue;
-      int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-      int ncol = nda + ndb;
-      int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
-      const T* J = cr + CR_J;
-      for (int e = LANE; e < ncol * ncol; e += WAVE) {
-        int ii = e / ncol, jj = e % ncol;
-        T b0 = J[ii], b1 = J[CJ + ii], b2 = J[2 * CJ + ii];
-        T k0 = Kc[0] * J[jj] + Kc[3] * J[CJ + jj] + Kc[4] * J[2 * CJ + jj];
-        T k1 = Kc[3] * J[jj] + Kc[1] * J[CJ + jj] + Kc[5] * J[2 * CJ + jj];
-        T k2 = Kc[4] * J[jj] + Kc[5] * J[CJ + jj] + Kc[2] * J[2 * CJ + jj];
-        int gi = ii < nda ? oa + ii : ob + ii - nda;
-        int gj = jj < nda ? oa + jj : ob + jj - nda;
-        H[gi * nv + gj] += b0 * k0 + b1 * k1 + b2 * k2;
+      int incl = sz;
+#pragma unroll
+      for (int o = 1; o < WAVE; o <<= 1) {
+        int y = __shfl_up(incl, o);
+        if (LANE >= o) incl += y;
+      }
+      const int total = __shfl(incl, WAVE - 1);
+      int* hoff = w.misc() + 16;  // [64] exclusive block offsets (misc has room, see lds layout)
+      if (LANE < ncon) hoff[LANE] = incl - sz;
+      SYNC();
+      for (int e0 = 0; e0 < total; e0 += WAVE) {
+        const int e = e0 + LANE;
+        if (e < total) {
+          int lo = 0, hi = ncon - 1;
+          while (lo < hi) {
+            int mid = (lo + hi + 1) >> 1;
+            if (hoff[mid] <= e)
+              lo = mid;
+            else
+              hi = mid - 1;
+          }
+          const int* ci = w.ci() + 4 * lo;
+          const T* cr = w.cr() + CR_N * lo;
+          const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+          const int ncol = nda + ndb;
+          const int loc = e - hoff[lo];
+          const int ii = loc / ncol, jj = loc - ii * ncol;
+          const T* J = cr + CR_J;
+          const T* Kc = cr + CR_K;
+          T b0 = J[ii], b1 = J[CJ + ii], b2 = J[2 * CJ + ii];
+          T k0 = Kc[0] * J[jj] + Kc[3] * J[CJ + jj] + Kc[4] * J[2 * CJ + jj];
+          T k1 = Kc[3] * J[jj] + Kc[1] * J[CJ + jj] + Kc[5] * J[2 * CJ + jj];
+          T k2 = Kc[4] * J[jj] + Kc[5] * J[CJ + jj] + Kc[2] * J[2 * CJ + jj];
+          const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+          const int gi = ii < nda ? oa + ii : ob + ii - nda;
+          const int gj = jj < nda ? oa + jj : ob + jj - nda;
+          atomicAdd(H + gi * nv + gj, b0 * k0 + b1 * k1 + b2 * k2);
+        }
       }
       SYNC();
     }
@@ -2591,6 +2646,7 @@ __device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T, DIM>&
   }
   SYNC();
   if (LANE == 0) task_reset<T, DIM>(M, q, v, ti, td, w.ctrl());
+  FULL_SYNC();
   SYNC();
   stage(M, w, arena, ctr);
   smooth_acc(M, w, arena, false);
@@ -2636,6 +2692,7 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
     ti[2 * dm.K + I_EPLEN] = 0;
   }
   SYNC();
+  FULL_SYNC();
   if (obs) write_obs(M, w, ti, obs + (size_t)arena * dm.obs_dim);
 }
 
@@ -2750,6 +2807,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
     for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
     if (LANE == 0) task_tail(M, w, ti, td, rng, ctr, act);
+    FULL_SYNC();
     SYNC();
     const int term = sc_[1] != 0.0;
     if (LANE == 0) {
@@ -2780,6 +2838,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     if (!term) break;
     // ---- auto-reset (reset_sim, base_env.py:177-198): terminal obs, zero state, TaskManager.reset,
     // then one more pass of this loop = the forward at the reset state that leaves qacc_warmstart
+    FULL_SYNC();
     if (io.terminal_obs) write_obs(M, w, ti, io.terminal_obs + (size_t)arena * dm.obs_dim);
     SYNC();
     for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = T(0);
@@ -2799,6 +2858,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     reset_pass = true;
   }
   store_state(M, S, w, arena);
+  FULL_SYNC();
   if (io.obs) write_obs(M, w, ti, io.obs + (size_t)arena * dm.obs_dim);
   PMARK(PH_TAIL);
   if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);
