@@ -6,6 +6,46 @@
 
 namespace fm {
 
+// Address-space-tagged device pointers.  Launch parameters reach the kernel through an opaque kernarg
+// pointer (see step_kernel), which hides from the compiler where the pointers stored in them point; a
+// plain pointer would then be accessed with FLAT instructions (which count against both vmcnt and
+// lgkmcnt, so every table read also drains the wave's LDS traffic).  cptr<X> (read-only scene tables,
+// actions) round-trips through the constant address space -> scalar loads for uniform indices and
+// global_load otherwise; gptr<X> (state, outputs) through the global address space -> global_load/store.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FM_AS_CONST __attribute__((address_space(4)))
+#define FM_AS_GLOBAL __attribute__((address_space(1)))
+#else
+#define FM_AS_CONST
+#define FM_AS_GLOBAL
+#endif
+template <typename X>
+struct cptr {
+  const X* p;
+  cptr() = default;
+  __host__ __device__ constexpr cptr(const X* q) : p(q) {}
+  __host__ __device__ __forceinline__ operator const X*() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (const X*)(const X FM_AS_CONST*)p;
+#else
+    return p;
+#endif
+  }
+};
+template <typename X>
+struct gptr {
+  X* p;
+  gptr() = default;
+  __host__ __device__ constexpr gptr(X* q) : p(q) {}
+  __host__ __device__ __forceinline__ operator X*() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (X*)(X FM_AS_GLOBAL*)p;
+#else
+    return p;
+#endif
+  }
+};
+
 constexpr int WAVE = 64;
 constexpr int MAXCON = 64;    // per-arena contact capacity (64-bit tree masks)
 constexpr int CJ = 18;        // Jacobian columns per contact (two trees of <= 9 dofs)
@@ -38,55 +78,55 @@ struct Model {
   int env_class, solver_iter;
   double solver_tol;
   // arm template
-  const T* arm_base;  // [A][12]  world pos(3), R(9) of the iiwa frame
-  const T* body;      // [10][32] local pos(3) local R(9) mass ipos(3) iR(9) I(3) invw_t invw_r pad(2)
-  const T* dof;       // [9][4]   range lo, hi, dof_invweight0, pad
-  const T* ctrlrange; // [nu][2]
+  cptr<T> arm_base;  // [A][12]  world pos(3), R(9) of the iiwa frame
+  cptr<T> body;      // [10][32] local pos(3) local R(9) mass ipos(3) iR(9) I(3) invw_t invw_r pad(2)
+  cptr<T> dof;       // [9][4]   range lo, hi, dof_invweight0, pad
+  cptr<T> ctrlrange; // [nu][2]
   // geoms (compact, collidable)
-  const T* geom;      // [ngc][16]  pos(3) R(9) size(3) rbound
-  const int* geom_i;  // [ngc][4]   mjid, type, kbody, box slot
-  const uint32_t* pair;  // [npair]  c1 | c2 << 12 | param << 24 (reference list; the kernel uses cb*)
-  const int* ginfo;      // [ngc] packed: type code | arm << 2 | pclass << 3 | kbody << 8
-  const int* cbi;        // [ncb][4] kbody, flags, first index in cbg, geom count
-  const T* cbs;          // [ncb][8] static AABB centre(3), radius, half extents(3), pad
-  const uint16_t* cbg;   // geoms grouped by collision body
-  const uint32_t* cbp;   // [ncbp] allowed collision-body pairs b1 | b2 << 8
+  cptr<T> geom;      // [ngc][16]  pos(3) R(9) size(3) rbound
+  cptr<int> geom_i;  // [ngc][4]   mjid, type, kbody, box slot
+  cptr<uint32_t> pair;  // [npair]  c1 | c2 << 12 | param << 24 (reference list; the kernel uses cb*)
+  cptr<int> ginfo;      // [ngc] packed: type code | arm << 2 | pclass << 3 | kbody << 8
+  cptr<int> cbi;        // [ncb][4] kbody, flags, first index in cbg, geom count
+  cptr<T> cbs;          // [ncb][8] static AABB centre(3), radius, half extents(3), pad
+  cptr<uint16_t> cbg;   // geoms grouped by collision body
+  cptr<uint32_t> cbp;   // [ncbp] allowed collision-body pairs b1 | b2 << 8
   int ptab[25];          // param index by (pclass g1, pclass g2)
-  const T* param;     // [nparam][8] mu, solref(2), solimp(5)
+  cptr<T> param;     // [nparam][8] mu, solref(2), solimp(5)
   // per arena
-  const T* cube;      // [N][K][4] h, m, I, pad
-  const T* meaninertia;  // [N]
-  const uint32_t* tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
+  cptr<T> cube;      // [N][K][4] h, m, I, pad
+  cptr<T> meaninertia;  // [N]
+  cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
   int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one
 };
 
 template <typename T>
 struct State {
-  T* phys;
-  double* dbl;
-  int32_t* ints;
-  uint64_t* rng;      // [N][4]
-  int64_t* counters;  // [N][4]
+  gptr<T> phys;
+  gptr<double> dbl;
+  gptr<int32_t> ints;
+  gptr<uint64_t> rng;      // [N][4]
+  gptr<int64_t> counters;  // [N][4]
 };
 
 struct StepIO {
-  const float* actions;
-  float* obs;
-  float* reward;
-  uint8_t* terminated;
-  uint8_t* truncated;
-  int32_t* scores;
-  int32_t* num_obj;
-  double* play_time;
-  double* conveyor_speed;
-  uint8_t* out_of_reach;
-  uint8_t* force_terminate;
-  float* terminal_obs;
-  double* ep_return;
-  int32_t* ep_len;
-  int32_t* terminal_scores;
-  const uint8_t* reset_mask;
+  cptr<float> actions;
+  gptr<float> obs;
+  gptr<float> reward;
+  gptr<uint8_t> terminated;
+  gptr<uint8_t> truncated;
+  gptr<int32_t> scores;
+  gptr<int32_t> num_obj;
+  gptr<double> play_time;
+  gptr<double> conveyor_speed;
+  gptr<uint8_t> out_of_reach;
+  gptr<uint8_t> force_terminate;
+  gptr<float> terminal_obs;
+  gptr<double> ep_return;
+  gptr<int32_t> ep_len;
+  gptr<int32_t> terminal_scores;
+  cptr<uint8_t> reset_mask;
 };
 
 // opaque copy of a pointer: loads through the result cannot be CSE'd with, or hoisted above, earlier
@@ -95,6 +135,14 @@ template <typename P>
 __device__ __forceinline__ const P* opaque(const P* p) {
   asm volatile("" : "+s"(p));
   return p;
+}
+
+// the kernel's own parameter block, through a fresh opaque constant-address-space pointer at each use
+template <typename P>
+__device__ __forceinline__ const P& kparams() {
+  const P FM_AS_CONST* p = (const P FM_AS_CONST*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const P*)p;
 }
 
 // LDS base with an opaque zero VGPR added: every workspace access becomes [vbase + immediate offset]
@@ -116,7 +164,7 @@ struct Lay {
   int alen, avel, aforce;
   int bpos, bR, bcom, bIw, bF, bN, dax, danc, site;
   int cR;
-  int Marm, Larm, LBarm;
+  int Marm;
   int gx;     // T [ngc][4]  geom world centre, rbound
   int ginfo, cbi, cbw, cbg;  // LDS copies of the geom / collision-body tables, body bounds T [ncb][8]
   int sp, spoff, gsurv;      // broadphase work lists
@@ -278,8 +326,8 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.cbi = take(4 * 4 * ncb);
   L.cbg = take(2 * ngc);
   L.cube = take(tsize * 4 * K);
-  // phase-local buffers share one region: collision work lists (stage), the arm-block factor
-  // (smooth acceleration / integration) and the Newton Hessian (solve) are never live together
+  // phase-local buffers share one region: collision work lists (stage) and the Newton Hessian (solve)
+  // are never live together
   const int u0 = off;
   L.H = take(tsize * nv * nv);
   int uend = off;
@@ -293,10 +341,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.skey = take(4 * maxcon);
   L.spw = take(4 * maxcon);
   uend = off > uend ? off : uend;
-  off = u0;
-  L.Larm = take(tsize * 81 * A);
-  L.LBarm = L.Larm;
-  off = off > uend ? off : uend;
+  off = uend;
   L.c_i = take(4 * 4 * maxcon);
   L.c_r = take(tsize * CR_N * maxcon);
   L.r_i = take(4 * 4 * maxrow);

@@ -266,22 +266,6 @@ struct Ws {
       return (T*)(base + L->Marm);
     }
   }
-  __device__ __forceinline__ T* Larm() const {
-    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
-      constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.Larm);
-    } else {
-      return (T*)(base + L->Larm);
-    }
-  }
-  __device__ __forceinline__ T* LBarm() const {
-    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
-      constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.LBarm);
-    } else {
-      return (T*)(base + L->LBarm);
-    }
-  }
   __device__ __forceinline__ T* gx() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -1691,32 +1675,39 @@ __device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T, DIM>& w, int
   }
 }
 
-// in-place 9x9 Cholesky (lower), one lane
+// 9x9 SPD solve A x = b on one lane with A's lower triangle (packed row-major, P9(i,j) = i(i+1)/2 + j)
+// held in registers (right-looking factor, then forward and backward substitution)
+__host__ __device__ constexpr int P9(int i, int j) { return i * (i + 1) / 2 + j; }
 template <typename T>
-__device__ __forceinline__ void chol9(T* A) {
+__device__ __forceinline__ void spd9_solve(T (&A)[45], T (&x)[9]) {
+#pragma unroll
   for (int j = 0; j < 9; j++) {
-    T s = A[9 * j + j];
-    for (int k = 0; k < j; k++) s -= A[9 * j + k] * A[9 * j + k];
-    T l = sqrt(s > T(1e-300) ? s : T(1e-300));
-    A[9 * j + j] = l;
+    T s = A[P9(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; k++) s -= A[P9(j, k)] * A[P9(j, k)];
+    const T l = sqrt(s > T(1e-300) ? s : T(1e-300));
+    A[P9(j, j)] = l;
+#pragma unroll
     for (int i = j + 1; i < 9; i++) {
-      T t = A[9 * i + j];
-      for (int k = 0; k < j; k++) t -= A[9 * i + k] * A[9 * j + k];
-      A[9 * i + j] = t / l;
+      T t = A[P9(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= A[P9(i, k)] * A[P9(j, k)];
+      A[P9(i, j)] = t / l;
     }
   }
-}
-template <typename T>
-__device__ __forceinline__ void cholsolve9(const T* L, T* x) {
+#pragma unroll
   for (int i = 0; i < 9; i++) {
     T t = x[i];
-    for (int k = 0; k < i; k++) t -= L[9 * i + k] * x[k];
-    x[i] = t / L[9 * i + i];
+#pragma unroll
+    for (int k = 0; k < i; k++) t -= A[P9(i, k)] * x[k];
+    x[i] = t / A[P9(i, i)];
   }
+#pragma unroll
   for (int i = 8; i >= 0; i--) {
     T t = x[i];
-    for (int k = i + 1; k < 9; k++) t -= L[9 * k + i] * x[k];
-    x[i] = t / L[9 * i + i];
+#pragma unroll
+    for (int k = i + 1; k < 9; k++) t -= A[P9(k, i)] * x[k];
+    x[i] = t / A[P9(i, i)];
   }
 }
 
@@ -2269,12 +2260,16 @@ __device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T, DIM>& 
   int a0 = 1 + 6 * K;
   for (int i = LANE; i < a0; i += WAVE) w.as()[i] = w.fs()[i] / Mdiag(M, w, i);
   if (LANE < dm.A) {
-    T* L = w.Larm() + 81 * LANE;
-    for (int k = 0; k < 81; k++) L[k] = w.Marm()[81 * LANE + k];
-    chol9(L);
-    T x[9];
-    for (int k = 0; k < 9; k++) x[k] = w.fs()[a0 + 9 * LANE + k];
-    cholsolve9(L, x);
+    const T* Mb = w.Marm() + 81 * LANE;
+    T Lp[45], x[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#pragma unroll
+      for (int j = 0; j <= i; j++) Lp[P9(i, j)] = Mb[9 * i + j];
+      x[i] = w.fs()[a0 + 9 * LANE + i];
+    }
+    spd9_solve(Lp, x);
+#pragma unroll
     for (int k = 0; k < 9; k++) w.as()[a0 + 9 * LANE + k] = x[k];
   }
   SYNC();
@@ -2296,23 +2291,27 @@ __device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T
   }
   for (int i = 1 + LANE; i < a0; i += WAVE) acc[i] = (w.fs()[i] + w.fc()[i]) / Mdiag(M, w, i);
   if (LANE < dm.A) {
-    T* L = w.LBarm() + 81 * LANE;
-    for (int k = 0; k < 81; k++) L[k] = w.Marm()[81 * LANE + k];
+    const T* Mb = w.Marm() + 81 * LANE;
+    T Lp[45], x[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#pragma unroll
+      for (int j = 0; j <= i; j++) Lp[P9(i, j)] = Mb[9 * i + j];
+      x[i] = w.fs()[a0 + 9 * LANE + i] + w.fc()[a0 + 9 * LANE + i];
+    }
     if (actuation) {
-      for (int j = 0; j < 7; j++) L[9 * j + j] += dt * T(200);
+#pragma unroll
+      for (int j = 0; j < 7; j++) Lp[P9(j, j)] += dt * T(200);
       T fg = w.aforce()[1 + 8 * LANE + 7];
       if (fg > T(-100) && fg < T(100)) {
         T d = dt * T(10) * T(0.25);
-        L[9 * 7 + 7] += d;
-        L[9 * 8 + 8] += d;
-        L[9 * 7 + 8] += d;
-        L[9 * 8 + 7] += d;
+        Lp[P9(7, 7)] += d;
+        Lp[P9(8, 8)] += d;
+        Lp[P9(8, 7)] += d;
       }
     }
-    chol9(L);
-    T x[9];
-    for (int k = 0; k < 9; k++) x[k] = w.fs()[a0 + 9 * LANE + k] + w.fc()[a0 + 9 * LANE + k];
-    cholsolve9(L, x);
+    spd9_solve(Lp, x);
+#pragma unroll
     for (int k = 0; k < 9; k++) acc[a0 + 9 * LANE + k] = x[k];
   }
   SYNC();
@@ -2435,7 +2434,8 @@ __device__ __forceinline__ void task_reset(const Model<T>& M, T* q, T* v, int32_
 }
 
 template <typename T, typename DIM>
-__device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr) {
+__device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr,
+                                         int* orig) {
   const DIM dm(M.dm);
   const int K = dm.K;
   int32_t* ins = ti;
@@ -2456,31 +2456,31 @@ __device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t*
     ts[I_SINCE] = 0;
   }
   if (ts[I_NIN] > 0) {
-    int n = ts[I_NIN];
-    bool oob[64];
-    for (int i = 0; i < n; i++) {
+    // out of bounds (task_utils.py:84-94): popping index i only shifts the entries above i, which the
+    // descending walk has already visited, so each test reads the position it would have read up front
+    for (int i = ts[I_NIN] - 1; i >= 0; i--) {
       const T* qq = q + 1 + 7 * ins[i];
-      double x = (double)qq[0], y = (double)qq[1], z = (double)qq[2];
-      oob[i] = fabs(x) > 1.2 || y < -1.5 || z < 0.9;
-    }
-    for (int i = n - 1; i >= 0; i--) {
-      if (!oob[i]) continue;
+      const double x = (double)qq[0], y = (double)qq[1], z = (double)qq[2];
+      if (!(fabs(x) > 1.2 || y < -1.5 || z < 0.9)) continue;
       int obj = ins[i];
       pop_at(ins, &ts[I_NIN], i);
       hide_cube(dm, q, v, ti, obj);
       ts[I_FAIL]++;
     }
     if (ts[I_NIN] > 0) {
-      int n2 = ts[I_NIN];
-      double pos[64][3];
-      for (int i = 0; i < n2; i++)
-        for (int c = 0; c < 3; c++) pos[i][c] = (double)q[1 + 7 * ins[i] + c];
+      // buckets (task_utils.py:99-113): positions are captured once for both buckets (obj_pos), indices
+      // into the shrinking list are reused.  orig[] keeps the captured order; a cube popped for bucket 0
+      // is parked at x = 5 and lay inside bucket 0 before, so its current and captured positions both
+      // fail bucket 1's test
+      const int n2 = ts[I_NIN];
+      for (int i = 0; i < n2; i++) orig[i] = ins[i];
       for (int b = 0; b < 2; b++) {
         double bx = b == 0 ? M.bucket_x0 : M.bucket_x1, by = M.bucket_y, bz = M.bucket_z;
         for (int i = n2 - 1; i >= 0; i--) {
-          bool in_x = fabs(pos[i][0] - bx) <= 0.6 * 0.29;
-          bool in_y = fabs(pos[i][1] - by) <= 0.6 * 0.29;
-          bool in_z = pos[i][2] - bz - 0.02 / 2 <= 0.07;
+          const T* qq = q + 1 + 7 * orig[i];
+          bool in_x = fabs((double)qq[0] - bx) <= 0.6 * 0.29;
+          bool in_y = fabs((double)qq[1] - by) <= 0.6 * 0.29;
+          bool in_z = (double)qq[2] - bz - 0.02 / 2 <= 0.07;
           if (!(in_x && in_y && in_z)) continue;
           if (i >= ts[I_NIN]) {  // reference: IndexError (task_utils.py:103-113 index reuse)
             ctr[3] += 1;
@@ -2509,7 +2509,7 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
   double* sc = w.scal();
-  int fail = task_step<T, DIM>(M, w.q(), w.v(), ti, td, rng, ctr);
+  int fail = task_step<T, DIM>(M, w.q(), w.v(), ti, td, rng, ctr, w.sortidx());
   double dt_env = 0.001 * dm.frame_skip;
   td[2] += dt_env;
   td[1] += M.accel * dt_env;
@@ -2702,11 +2702,11 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   (void)params;
   // All launch parameters are read through an opaque pointer to the kernarg segment at each use, so the
   // compiler cannot hoist the ~50 scalar values out of the substep loop and run out of SGPRs.
-  const StepParams<T>* PK = (const StepParams<T>*)__builtin_amdgcn_kernarg_segment_ptr();
-#define M (opaque(PK)->M)
-#define S (opaque(PK)->S)
-#define io (opaque(PK)->io)
-#define L (opaque(PK)->L)
+  // The pointer stays in the constant address space (scalar loads, no FLAT instructions).
+#define M (kparams<StepParams<T>>().M)
+#define S (kparams<StepParams<T>>().S)
+#define io (kparams<StepParams<T>>().io)
+#define L (kparams<StepParams<T>>().L)
   const int arena = blockIdx.x;
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K, nu = dm.nu;
