@@ -1728,6 +1728,56 @@ __device__ __forceinline__ double readlane(double x, int l) {
 __device__ __forceinline__ float lane_bcast(float x, int l) { return readlane(x, l); }
 __device__ __forceinline__ double lane_bcast(double x, int l) { return __shfl(x, l); }
 
+// fp32 variant: the trailing-update operands L[i][k] are broadcast with v_readlane straight into SGPRs
+// (one VALU op each, no LDS round trip per pivot); the pivot itself is read the same way
+template <int NVM>
+__device__ __forceinline__ void chol_solve_rl(const float* H, int nv, const float* g, float* dir) {
+  const int j = LANE;
+  const float tiny = 1e-37f;
+  float col[NVM];
+#pragma unroll
+  for (int i = 0; i < NVM; i++) col[i] = (i < nv && j < nv) ? H[i * nv + j] : 0.0f;
+  SYNC();
+  float dinv = 1.0f;
+#pragma unroll
+  for (int k = 0; k < NVM; k++) {
+    if (k < nv) {
+      float d = readlane(col[k], k);
+      d = d > tiny ? d : tiny;
+      const float ri = 1.0f / sqrtf(d);
+      const float lj = col[k] * ri;  // lane j >= k: L[j][k]
+      if (j == k) dinv = ri;
+      if (j >= k) col[k] = lj;
+      if (j > k) {
+#pragma unroll
+        for (int i = k + 1; i < NVM; i++)
+          if (i < nv) col[i] -= readlane(lj, i) * lj;
+      }
+    }
+  }
+  float acc = j < nv ? -g[j] : 0.0f;
+  float y = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NVM; k++) {
+    if (k < nv) {
+      const float yk = readlane(acc * dinv, k);
+      if (j == k) y = yk;
+      if (j > k) acc -= col[k] * yk;
+    }
+  }
+  float acc2 = y, x = 0.0f;
+#pragma unroll
+  for (int k = NVM - 1; k >= 0; k--) {
+    if (k < nv) {
+      const float xk = readlane(acc2 * dinv, k);
+      if (j == k) x = xk;
+      if (j < k) acc2 -= col[k] * dinv * xk;
+    }
+  }
+  if (j < nv) dir[j] = x;
+  SYNC();
+}
+
 template <typename T, int NVM>
 __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const T* g, T* dir) {
   const int j = LANE;
@@ -2046,7 +2096,10 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SYNC();
     PMARK(PH_NHESS);
     if (nv <= 48 && !(M.dbg_flags & 1)) {
-      chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
+      if constexpr (sizeof(T) == 4 && DIM::fixed)
+        chol_solve_rl<48>(H, nv, g, dir);
+      else
+        chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
       PMARK(PH_NCHOL);
     } else if (nv <= 64 && !(M.dbg_flags & 1)) {
       chol_solve_reg<T, 64>(H, w.bc(), nv, g, dir);
