@@ -177,6 +177,12 @@ static int create_typed(fm_handle* h) {
     for (int k = 0; k < 3; k++) o[25 + k] = s.body_I[b][k];
     o[28] = s.body_invw[b][0];
     o[29] = s.body_invw[b][1];
+    // the kernel folds ARM_BODY (fm_arm_table.hpp, generated at build time) into immediates: the scene
+    // compiled now must be the one the library was built with
+    for (int k = 0; k < 30; k++)
+      if (o[k] != ARM_BODY[b][k]) {
+        return set_err(FM_EINVAL, "arm template differs from the constants compiled into the kernel (rebuild)");
+      }
   }
   for (int j = 0; j < ARM_ND; j++) {
     dof[4 * j] = s.dof_range[j][0];

@@ -271,6 +271,32 @@ __device__ __forceinline__ T wave_max(T x) {
   return x;
 }
 
+// fp32 wave reductions on DPP (row quad-perms / rotates, then the row broadcasts) instead of ds_swizzle /
+// ds_bpermute: a VALU-latency chain, no LDS round trips.  The result is read from lane 63 (uniform).
+// Every call site runs with the full wave active (EXEC = all 64 lanes).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  x += dpp_f32<0xb1>(x, 0.0f);   // quad_perm [1,0,3,2]
+  x += dpp_f32<0x4e>(x, 0.0f);   // quad_perm [2,3,0,1]
+  x += dpp_f32<0x124>(x, 0.0f);  // row_ror:4
+  x += dpp_f32<0x128>(x, 0.0f);  // row_ror:8
+  x += dpp_f32<0x142>(x, 0.0f);  // row_bcast:15
+  x += dpp_f32<0x143>(x, 0.0f);  // row_bcast:31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+__device__ __forceinline__ float wave_min(float x) {
+  x = fminf(x, dpp_f32<0xb1>(x, x));
+  x = fminf(x, dpp_f32<0x4e>(x, x));
+  x = fminf(x, dpp_f32<0x124>(x, x));
+  x = fminf(x, dpp_f32<0x128>(x, x));
+  x = fminf(x, dpp_f32<0x142>(x, x));
+  x = fminf(x, dpp_f32<0x143>(x, x));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
 template <typename T>
 struct StepParams {
   Model<T> M;

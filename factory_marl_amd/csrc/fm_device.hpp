@@ -31,6 +31,7 @@
 #include "../../include/factorysim.h"
 #include "fm_dev.hpp"
 #include "fm_scene.hpp"
+#include "fm_arm_table.hpp"  // generated (gen_tables.cpp)
 
 #ifndef FM_WS_RUNTIME_LAYOUT
 #define FM_WS_RUNTIME_LAYOUT 0
@@ -1152,11 +1153,44 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
 // ------------------------------------------------------------------------------------------------
 // stage (mj_step1): kinematics, inertia, bias forces, collision, constraint rows, efc velocities
 // ------------------------------------------------------------------------------------------------
-template <typename T, typename DIM>
-__device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w, int arm, bool with_dyn) {
+// ---- arm template constants (fm_arm_table.hpp, generated from fm_scene.cpp): with the body loop unrolled
+// every table entry is an immediate; products with an exact 0 drop out and products with an exact +-1
+// become copies (the same value the full product gives), so the chain carries only the real arithmetic
+template <typename T>
+__device__ __forceinline__ T cmul(T x, double c) {
+  return c == 0.0 ? T(-0.0) : (T(c) == T(1) ? x : (T(c) == T(-1) ? -x : x * T(c)));
+}
+// r = R v, R a runtime matrix, v a constant vector
+template <typename T>
+__device__ __forceinline__ void matvec3_c(const T* R, const double* v, T* r) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) r[i] = cmul(R[3 * i], v[0]) + cmul(R[3 * i + 1], v[1]) + cmul(R[3 * i + 2], v[2]);
+}
+// C = A B, A runtime, B constant
+template <typename T>
+__device__ __forceinline__ void matmul3_c(const T* A, const double* B, T* C) {
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      C[3 * i + j] = cmul(A[3 * i], B[j]) + cmul(A[3 * i + 1], B[3 + j]) + cmul(A[3 * i + 2], B[6 + j]);
+}
+
+// Forward kinematics (+ RNE when DYN) of one arm on one lane: link1..7 (hinges about local z), the gripper
+// base (welded), the two plates (slides along local x) -- iiwa14.xml:62-139, gripper.xml:9-42.  Body poses,
+// joint axes/anchors, coms, world inertias, gripper site to LDS; DYN adds the RNE bias forces (qacc = 0)
+// of the arm's 9 dofs (MuJoCo mj_rne with flg_acc = 0: cvel / cacc recursion then the backward sum).
+template <typename T, typename DIM, bool DYN>
+__device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w, int arm) {
   const DIM dm(M.dm);
-  const T* q = w.q() + 1 + 7 * dm.K + 9 * arm;
-  const T* qd = w.v() + 1 + 6 * dm.K + 9 * arm;
+  const T* qa = w.q() + 1 + 7 * dm.K + 9 * arm;
+  const T* va = w.v() + 1 + 6 * dm.K + 9 * arm;
+  T q[9], qd[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    q[k] = qa[k];
+    qd[k] = DYN ? va[k] : T(0);
+  }
   const T* base = M.arm_base + 12 * arm;
   T* bpos = w.bpos() + 30 * arm;
   T* bR = w.bR() + 90 * arm;
@@ -1167,13 +1201,17 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
   T* dax = w.dax() + 27 * arm;
   T* danc = w.danc() + 27 * arm;
   const T p0[3] = {base[0], base[1], base[2]};
-  // chain state of the current parent (link chain), saved state of the gripper base for the plates
   T Pp[3] = {base[0], base[1], base[2]}, PR[9];
+#pragma unroll
   for (int k = 0; k < 9; k++) PR[k] = base[3 + k];
   T Pw[3] = {0, 0, 0}, Pal[3] = {0, 0, 0}, Pvo[3] = {0, 0, 0}, Pao[3] = {0, 0, 0};
   T Gp[3], GR[9], Gw[3], Gal[3], Gvo[3], Gao[3];
+  T ax7[3], ax8[3];
+#pragma unroll
   for (int b = 0; b < 10; b++) {
+    const double* bl = ARM_BODY[b];
     if (b >= 8) {  // both plates hang off the gripper base
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         Pp[k] = Gp[k];
         Pw[k] = Gw[k];
@@ -1181,37 +1219,43 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
         Pvo[k] = Gvo[k];
         Pao[k] = Gao[k];
       }
+#pragma unroll
       for (int k = 0; k < 9; k++) PR[k] = GR[k];
     }
-    const T* bl = M.body + 32 * b;
     T off[3], Rpre[9];
-    matvec3(PR, bl, off);
-    matmul3(PR, bl + 3, Rpre);
+    matvec3_c(PR, bl, off);
+    matmul3_c(PR, bl + 3, Rpre);
     T o[3] = {Pp[0] + off[0], Pp[1] + off[1], Pp[2] + off[2]};
     T R[9];
     T wv[3] = {Pw[0], Pw[1], Pw[2]}, al[3] = {Pal[0], Pal[1], Pal[2]};
-    T vo[3], ao[3];
+    T vo[3] = {0, 0, 0}, ao[3] = {0, 0, 0};
+    T r[3], t1[3], t2[3], t3[3];
+    if (DYN) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) r[k] = o[k] - Pp[k];
+      cross3(Pw, r, t1);
+      cross3(Pal, r, t2);
+      cross3(Pw, t1, t3);
+    }
     if (b < 7) {
-      T ax[3] = {Rpre[2], Rpre[5], Rpre[8]};
+      const T ax[3] = {Rpre[2], Rpre[5], Rpre[8]};
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         dax[3 * b + k] = ax[k];
         danc[3 * b + k] = o[k];
       }
-      T s, c;
-      sincos_t(q[b], &s, &c);
-      // R = Rpre * Rz(q)
-      for (int r = 0; r < 3; r++) {
-        R[3 * r + 0] = Rpre[3 * r + 0] * c + Rpre[3 * r + 1] * s;
-        R[3 * r + 1] = -Rpre[3 * r + 0] * s + Rpre[3 * r + 1] * c;
-        R[3 * r + 2] = Rpre[3 * r + 2];
+      T sn, cs;
+      sincos_t(q[b], &sn, &cs);
+#pragma unroll
+      for (int rr = 0; rr < 3; rr++) {
+        R[3 * rr + 0] = Rpre[3 * rr + 0] * cs + Rpre[3 * rr + 1] * sn;
+        R[3 * rr + 1] = -Rpre[3 * rr + 0] * sn + Rpre[3 * rr + 1] * cs;
+        R[3 * rr + 2] = Rpre[3 * rr + 2];
       }
-      if (with_dyn) {
-        T r[3] = {o[0] - Pp[0], o[1] - Pp[1], o[2] - Pp[2]};
-        T t1[3], t2[3], t3[3], wa[3];
-        cross3(Pw, r, t1);
-        cross3(Pal, r, t2);
-        cross3(Pw, t1, t3);
+      if (DYN) {
+        T wa[3];
         cross3(Pw, ax, wa);
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           vo[k] = Pvo[k] + t1[k];
           ao[k] = Pao[k] + t2[k] + t3[k];
@@ -1220,68 +1264,79 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
         }
       }
     } else if (b == 7) {
+#pragma unroll
       for (int k = 0; k < 9; k++) R[k] = Rpre[k];
-      if (with_dyn) {
-        T r[3] = {o[0] - Pp[0], o[1] - Pp[1], o[2] - Pp[2]};
-        T t1[3], t2[3], t3[3];
-        cross3(Pw, r, t1);
-        cross3(Pal, r, t2);
-        cross3(Pw, t1, t3);
+      if (DYN) {
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           vo[k] = Pvo[k] + t1[k];
           ao[k] = Pao[k] + t2[k] + t3[k];
         }
       }
     } else {
-      int d = b - 1;  // dof 7 (left plate, body 8) / 8 (right plate, body 9)
-      T ax[3] = {Rpre[0], Rpre[3], Rpre[6]};
-      for (int k = 0; k < 3; k++) o[k] += ax[k] * q[d];
+      const int d = b - 1;  // dof 7 (left plate, body 8) / 8 (right plate, body 9)
+      const T ax[3] = {Rpre[0], Rpre[3], Rpre[6]};
+#pragma unroll
       for (int k = 0; k < 3; k++) {
+        o[k] += ax[k] * q[d];
         dax[3 * d + k] = ax[k];
         danc[3 * d + k] = o[k];
+        if (d == 7)
+          ax7[k] = ax[k];
+        else
+          ax8[k] = ax[k];
       }
+#pragma unroll
       for (int k = 0; k < 9; k++) R[k] = Rpre[k];
-      if (with_dyn) {
-        T r[3] = {o[0] - Pp[0], o[1] - Pp[1], o[2] - Pp[2]};
-        T t1[3], t2[3], t3[3], wa[3];
+      if (DYN) {
+        // r includes the slide displacement
+#pragma unroll
+        for (int k = 0; k < 3; k++) r[k] = o[k] - Pp[k];
         cross3(Pw, r, t1);
         cross3(Pal, r, t2);
         cross3(Pw, t1, t3);
+        T wa[3];
         cross3(Pw, ax, wa);
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           vo[k] = Pvo[k] + t1[k] + ax[k] * qd[d];
           ao[k] = Pao[k] + t2[k] + t3[k] + T(2) * wa[k] * qd[d];
         }
       }
     }
+#pragma unroll
     for (int k = 0; k < 3; k++) bpos[3 * b + k] = o[k];
+#pragma unroll
     for (int k = 0; k < 9; k++) bR[9 * b + k] = R[k];
     // com and world inertia
     T ci[3];
-    matvec3(R, bl + 13, ci);
+    matvec3_c(R, bl + 13, ci);
     T com[3] = {o[0] + ci[0], o[1] + ci[1], o[2] + ci[2]};
+#pragma unroll
     for (int k = 0; k < 3; k++) bcom[3 * b + k] = com[k];
     T Ri[9];
-    matmul3(R, bl + 16, Ri);
-    const T* I = bl + 25;
+    matmul3_c(R, bl + 16, Ri);
+    const double* I = bl + 25;
     T Iw[6];
-    Iw[0] = Ri[0] * I[0] * Ri[0] + Ri[1] * I[1] * Ri[1] + Ri[2] * I[2] * Ri[2];
-    Iw[1] = Ri[3] * I[0] * Ri[3] + Ri[4] * I[1] * Ri[4] + Ri[5] * I[2] * Ri[5];
-    Iw[2] = Ri[6] * I[0] * Ri[6] + Ri[7] * I[1] * Ri[7] + Ri[8] * I[2] * Ri[8];
-    Iw[3] = Ri[0] * I[0] * Ri[3] + Ri[1] * I[1] * Ri[4] + Ri[2] * I[2] * Ri[5];
-    Iw[4] = Ri[0] * I[0] * Ri[6] + Ri[1] * I[1] * Ri[7] + Ri[2] * I[2] * Ri[8];
-    Iw[5] = Ri[3] * I[0] * Ri[6] + Ri[4] * I[1] * Ri[7] + Ri[5] * I[2] * Ri[8];
+    Iw[0] = cmul(Ri[0] * Ri[0], I[0]) + cmul(Ri[1] * Ri[1], I[1]) + cmul(Ri[2] * Ri[2], I[2]);
+    Iw[1] = cmul(Ri[3] * Ri[3], I[0]) + cmul(Ri[4] * Ri[4], I[1]) + cmul(Ri[5] * Ri[5], I[2]);
+    Iw[2] = cmul(Ri[6] * Ri[6], I[0]) + cmul(Ri[7] * Ri[7], I[1]) + cmul(Ri[8] * Ri[8], I[2]);
+    Iw[3] = cmul(Ri[0] * Ri[3], I[0]) + cmul(Ri[1] * Ri[4], I[1]) + cmul(Ri[2] * Ri[5], I[2]);
+    Iw[4] = cmul(Ri[0] * Ri[6], I[0]) + cmul(Ri[1] * Ri[7], I[1]) + cmul(Ri[2] * Ri[8], I[2]);
+    Iw[5] = cmul(Ri[3] * Ri[6], I[0]) + cmul(Ri[4] * Ri[7], I[1]) + cmul(Ri[5] * Ri[8], I[2]);
+#pragma unroll
     for (int k = 0; k < 6; k++) bIw[6 * b + k] = Iw[k];
-    if (with_dyn) {
-      T mass = bl[12];
-      T rc[3] = {com[0] - o[0], com[1] - o[1], com[2] - o[2]};
+    if (DYN) {
+      const double mass = bl[12];
+      const T rc[3] = {com[0] - o[0], com[1] - o[1], com[2] - o[2]};
       T u1[3], u2[3], u3[3];
       cross3(al, rc, u1);
       cross3(wv, rc, u2);
       cross3(wv, u2, u3);
       T F[3];
-      for (int k = 0; k < 3; k++) F[k] = mass * (ao[k] + u1[k] + u3[k]);
-      F[2] += mass * M.grav;
+#pragma unroll
+      for (int k = 0; k < 3; k++) F[k] = cmul(ao[k] + u1[k] + u3[k], mass);
+      F[2] += T(mass) * M.grav;
       T Iwv[3] = {Iw[0] * wv[0] + Iw[3] * wv[1] + Iw[4] * wv[2], Iw[3] * wv[0] + Iw[1] * wv[1] + Iw[5] * wv[2],
                   Iw[4] * wv[0] + Iw[5] * wv[1] + Iw[2] * wv[2]};
       T Ial[3] = {Iw[0] * al[0] + Iw[3] * al[1] + Iw[4] * al[2], Iw[3] * al[0] + Iw[1] * al[1] + Iw[5] * al[2],
@@ -1290,15 +1345,19 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
       cross3(wv, Iwv, gy);
       T cr[3] = {com[0] - p0[0], com[1] - p0[1], com[2] - p0[2]}, mo[3];
       cross3(cr, F, mo);
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         bF[3 * b + k] = F[k];
         bN[3 * b + k] = mo[k] + Ial[k] + gy[k];
       }
     }
     // advance the chain
+#pragma unroll
     for (int k = 0; k < 3; k++) Pp[k] = o[k];
+#pragma unroll
     for (int k = 0; k < 9; k++) PR[k] = R[k];
-    if (with_dyn) {
+    if (DYN) {
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         Pw[k] = wv[k];
         Pal[k] = al[k];
@@ -1307,6 +1366,7 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
       }
     }
     if (b == 7) {
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         Gp[k] = o[k];
         Gw[k] = Pw[k];
@@ -1314,20 +1374,26 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
         Gvo[k] = Pvo[k];
         Gao[k] = Pao[k];
       }
+#pragma unroll
       for (int k = 0; k < 9; k++) GR[k] = R[k];
       // between_gripper_plates site (gripper.xml:43)
-      T so[3] = {0, 0, T(0.05)}, sp[3];
-      matvec3(R, so, sp);
+      T sp[3];
+      matvec3_c(R, ARM_GRIP_SITE, sp);
+#pragma unroll
       for (int k = 0; k < 3; k++) w.site()[3 * arm + k] = o[k] + sp[k];
     }
   }
-  if (with_dyn) {
-    // backward pass: generalized bias forces of the arm's 9 dofs (RNE, qacc = 0)
+  if (DYN) {
+    SYNC();
+    // backward pass: generalized bias forces of the arm's 9 dofs (RNE, qacc = 0); the per-body records
+    // come back from LDS in one batch of independent reads
     T* pb = w.pb() + 1 + 6 * dm.K + 9 * arm;
-    pb[7] = -(dax[21] * bF[24] + dax[22] * bF[25] + dax[23] * bF[26]);
-    pb[8] = -(dax[24] * bF[27] + dax[25] * bF[28] + dax[26] * bF[29]);
+    pb[7] = -(ax7[0] * bF[24] + ax7[1] * bF[25] + ax7[2] * bF[26]);
+    pb[8] = -(ax8[0] * bF[27] + ax8[1] * bF[28] + ax8[2] * bF[29]);
     T ft[3] = {0, 0, 0}, nt[3] = {0, 0, 0};
+#pragma unroll
     for (int b = 9; b >= 0; b--) {
+#pragma unroll
       for (int k = 0; k < 3; k++) {
         ft[k] += bF[3 * b + k];
         nt[k] += bN[3 * b + k];
@@ -1395,7 +1461,7 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   T* q = w.q();
   T* v = w.v();
   // ---- kinematics + RNE (one lane per arm), cubes (one lane per cube)
-  if (LANE < A) arm_chain(M, w, LANE, true);
+  if (LANE < A) arm_chain<T, DIM, true>(M, w, LANE);
   for (int k = LANE; k < K; k += WAVE) {
     T* qq = q + 1 + 7 * k;
     T qu[4] = {qq[3], qq[4], qq[5], qq[6]};
@@ -1448,39 +1514,50 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     w.alen()[u] = L;
     w.avel()[u] = V;
   }
-  // ---- arm mass-matrix blocks: M_ij = sum_{b in desc} m Jc_i.Jc_j + Jr_i' Iw Jr_j
+  // ---- arm mass-matrix blocks: M_ij = sum_{b in desc} m Jc_i.Jc_j + Jr_i' Iw Jr_j, one entry (i >= j) per
+  // lane; the body loop is unrolled (masses are immediates, every LDS read independent), bodies outside the
+  // subtree of dof i are selected away
   for (int e = LANE; e < 45 * A; e += WAVE) {
-    int arm = e / 45, t = e % 45;
-    int i = 0;
-    while (t > i) {
-      t -= i + 1;
-      i++;
-    }
-    int j = t;  // i >= j
-    int b0, b1;
-    if (i <= 6) {
-      b0 = i;
-      b1 = 9;
-    } else {
-      b0 = b1 = i + 1;
-    }
-    T s = 0;
+    const int arm = e / 45;
+    const int t = e - 45 * arm;
+    int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);  // packed lower-triangle index -> (i, j)
+    if ((i + 1) * (i + 2) / 2 <= t) i++;
+    if (i * (i + 1) / 2 > t) i--;
+    const int j = t - i * (i + 1) / 2;
     const T* dax = w.dax() + 27 * arm;
-    for (int b = b0; b <= b1; b++) {
-      const T* com = w.bcom() + 30 * arm + 3 * b;
+    const T* danc = w.danc() + 27 * arm;
+    const T* bcom = w.bcom() + 30 * arm;
+    const T* bIw = w.bIw() + 60 * arm;
+    const T ai[3] = {dax[3 * i], dax[3 * i + 1], dax[3 * i + 2]}, aj[3] = {dax[3 * j], dax[3 * j + 1], dax[3 * j + 2]};
+    const T pi[3] = {danc[3 * i], danc[3 * i + 1], danc[3 * i + 2]};
+    const T pj[3] = {danc[3 * j], danc[3 * j + 1], danc[3 * j + 2]};
+    const bool hi_i = i <= 6, hi_j = j <= 6;
+    T s = 0;
+#pragma unroll
+    for (int b = 0; b < 10; b++) {
+      const bool in = (hi_i ? b >= i : b == i + 1) && (hi_j ? b >= j : b == j + 1);
+      const T* com = bcom + 3 * b;
+      const T* Iw = bIw + 6 * b;
+      const T ri[3] = {com[0] - pi[0], com[1] - pi[1], com[2] - pi[2]};
+      const T rj[3] = {com[0] - pj[0], com[1] - pj[1], com[2] - pj[2]};
       T ci[3], cj[3];
-      arm_jac_col(w, arm, b, i, com, ci);
-      arm_jac_col(w, arm, b, j, com, cj);
-      T mass = M.body[32 * b + 12];
-      s += mass * dot3(ci, cj);
-      if (i <= 6 && j <= 6) {
-        const T* Iw = w.bIw() + 60 * arm + 6 * b;
-        const T* ri = dax + 3 * i;
-        const T* rj = dax + 3 * j;
-        T Ir[3] = {Iw[0] * rj[0] + Iw[3] * rj[1] + Iw[4] * rj[2], Iw[3] * rj[0] + Iw[1] * rj[1] + Iw[5] * rj[2],
-                   Iw[4] * rj[0] + Iw[5] * rj[1] + Iw[2] * rj[2]};
-        s += dot3(ri, Ir);
+      cross3(ai, ri, ci);
+      cross3(aj, rj, cj);
+      if (!hi_i) {
+        ci[0] = ai[0];
+        ci[1] = ai[1];
+        ci[2] = ai[2];
       }
+      if (!hi_j) {
+        cj[0] = aj[0];
+        cj[1] = aj[1];
+        cj[2] = aj[2];
+      }
+      T term = T(ARM_BODY[b][12]) * dot3(ci, cj);
+      const T Ir[3] = {Iw[0] * aj[0] + Iw[3] * aj[1] + Iw[4] * aj[2], Iw[3] * aj[0] + Iw[1] * aj[1] + Iw[5] * aj[2],
+                       Iw[4] * aj[0] + Iw[5] * aj[1] + Iw[2] * aj[2]};
+      if (hi_i && hi_j) term += dot3(ai, Ir);
+      s += in ? term : T(0);
     }
     T* Ma = w.Marm() + 81 * arm;
     Ma[9 * i + j] = s;
@@ -1585,60 +1662,81 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     cr[CR_D] = T(1) / R;
     cr[CR_KD] = Kk * imp * dist;
     cr[CR_BD] = Bb;
-    // efc velocity in the contact frame
-    for (int r = 0; r < 3; r++) {
-      T s = 0;
-      for (int j = 0; j < nda; j++) s += J[r * CJ + j] * v[tree_dof(dm, ta) + j];
-      for (int j = 0; j < ndb; j++) s += J[r * CJ + nda + j] * v[tree_dof(dm, tb) + j];
-      cr[CR_VEL + r] = s;
-    }
   }
-  // ---- generic rows: gripper joint equality + active joint limits (lane 0)
-  if (LANE == 0) {
+  SYNC();
+  // efc velocity in the contact frame
+  contact_jx(M, w, v, ncon, CR_VEL);
+  // ---- generic rows: gripper joint equality + active joint limits.  One candidate row per lane in the
+  // reference's order (per arm: the equality, then each dof's lower and upper limit), compacted by ballot
+  {
+    constexpr int PER = 19;
+    const uint64_t below = (1ull << LANE) - 1ull;
     int nr = 0;
-    const T eq_sr[2] = {T(0.002), T(1.0)}, eq_si[5] = {T(0.98), T(0.9999), T(0.001), T(0.5), T(2.0)};
-    const T lim_sr[2] = {T(0.02), T(1.0)}, lim_si[5] = {T(0.9), T(0.95), T(0.001), T(0.5), T(2.0)};
-    for (int arm = 0; arm < A; arm++) {
-      int qa = 1 + 7 * K + 9 * arm, va = 1 + 6 * K + 9 * arm;
-      auto add = [&](int d0, T c0, int d1, T c1, T pos, T diag, const T* sr, const T* si) {
-        if (nr >= dm.maxrow) return;
-        int* ri = w.ri() + 4 * nr;
-        T* rr = w.rr() + RR_N * nr;
+    for (int c00 = 0; c00 < PER * A; c00 += WAVE) {
+      const int cand = c00 + LANE;
+      bool act = false, eq = false;
+      int d0 = 0, d1 = -1;
+      T c0 = 0, c1 = 0, pos = 0, diag = 0;
+      if (cand < PER * A) {
+        const int arm = cand / PER, k = cand - PER * arm;
+        const int qa = 1 + 7 * K + 9 * arm, va = 1 + 6 * K + 9 * arm;
+        if (k == 0) {  // gripper plates: q_left - q_right = 0 (gripper.xml:46-49)
+          act = eq = true;
+          d0 = va + 7;
+          d1 = va + 8;
+          c0 = T(1);
+          c1 = T(-1);
+          pos = q[qa + 7] - q[qa + 8];
+          diag = M.dof[4 * 7 + 2] + M.dof[4 * 8 + 2];
+        } else {
+          const int d = (k - 1) >> 1;
+          const bool upper = (k - 1) & 1;
+          const T qv = q[qa + d];
+          pos = upper ? M.dof[4 * d + 1] - qv : qv - M.dof[4 * d];
+          c0 = upper ? T(-1) : T(1);
+          act = pos < T(0);
+          d0 = va + d;
+          diag = M.dof[4 * d + 2];
+        }
+      }
+      const uint64_t bal = __ballot(act);
+      const int slot = nr + __popcll(bal & below);
+      if (act && slot < dm.maxrow) {
+        const T sr[2] = {eq ? T(0.002) : T(0.02), T(1.0)};
+        const T si[5] = {eq ? T(0.98) : T(0.9), eq ? T(0.9999) : T(0.95), T(0.001), T(0.5), T(2.0)};
+        int* ri = w.ri() + 4 * slot;
+        T* rr = w.rr() + RR_N * slot;
         ri[0] = d0;
         ri[1] = d1;
-        ri[2] = d1 >= 0 ? 0 : 1;  // 0 equality, 1 inequality
+        ri[2] = eq ? 0 : 1;  // 0 equality, 1 inequality
         rr[RR_C0] = c0;
         rr[RR_C1] = c1;
         rr[RR_POS] = pos;
-        T imp = impedance(si, pos);
+        const T imp = impedance(si, pos);
         T Kk, Bb;
         kb_params(M.dt, sr, si, Kk, Bb);
         T R = (T(1) - imp) * diag / imp;
         R = R > T(1e-15) ? R : T(1e-15);
         rr[RR_D] = T(1) / R;
-        T vel = c0 * v[d0] + (d1 >= 0 ? c1 * v[d1] : T(0));
+        const T vel = c0 * v[d0] + (d1 >= 0 ? c1 * v[d1] : T(0));
         rr[RR_AREF] = -Bb * vel - Kk * imp * pos;
-        nr++;
-      };
-      add(va + 7, T(1), va + 8, T(-1), q[qa + 7] - q[qa + 8], M.dof[4 * 7 + 2] + M.dof[4 * 8 + 2], eq_sr, eq_si);
-      for (int d = 0; d < 9; d++) {
-        T lo = M.dof[4 * d], hi = M.dof[4 * d + 1];
-        T dl = q[qa + d] - lo, dh = hi - q[qa + d];
-        if (dl < T(0)) add(va + d, T(1), -1, T(0), dl, M.dof[4 * d + 2], lim_sr, lim_si);
-        if (dh < T(0)) add(va + d, T(-1), -1, T(0), dh, M.dof[4 * d + 2], lim_sr, lim_si);
       }
+      nr += __popcll(bal);
     }
-    misc[MISC_NROW] = nr;
+    if (LANE == 0) misc[MISC_NROW] = nr < dm.maxrow ? nr : dm.maxrow;
   }
   SYNC();
-  // ---- tree -> contact masks
-  for (int t = LANE; t < dm.ntree; t += WAVE) {
-    uint64_t mk = 0;
-    for (int c = 0; c < ncon; c++) {
-      const int* ci = w.ci() + 4 * c;
-      if (ci[1] == t || ci[2] == t) mk |= 1ull << c;
+  // ---- tree -> contact masks: one ballot per tree over the contact lanes (ncon <= 64)
+  {
+    int ta = -2, tb = -2;
+    if (LANE < ncon) {
+      ta = w.ci()[4 * LANE + 1];
+      tb = w.ci()[4 * LANE + 2];
     }
-    w.tmask()[t] = mk;
+    for (int t = 0; t < dm.ntree; t++) {
+      const uint64_t mk = __ballot(ta == t || tb == t);
+      if (LANE == 0) w.tmask()[t] = mk;
+    }
   }
   (void)nv;
   SYNC();
@@ -1842,43 +1940,69 @@ __device__ __forceinline__ T edge_val(const T* x3, T mu, int e) {
   return x3[0] + ((e & 1) ? -mu : mu) * x3[1 + (e >> 1)];
 }
 
-// evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
+// contact-frame products B x for every contact: one lane per (contact, frame row), the <= 9 + 9 columns
+// unrolled with unconditional loads (x[o + j] stays inside the nv vector for every tree; columns past the
+// contact's own are selected away, never multiplied), result in the record's slot .. slot + 2
 template <typename T, typename DIM>
-__device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T, DIM>& w, const T* x, int ncon, int nrow) {
+__device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& w, const T* x, int ncon, int slot) {
   const DIM dm(M.dm);
-  T cst = 0;
-  for (int c = LANE; c < ncon; c += WAVE) {
+  for (int e = LANE; e < 3 * ncon; e += WAVE) {
+    const int c = e / 3, r = e - 3 * c;
     const int* ci = w.ci() + 4 * c;
     T* cr = w.cr() + CR_N * c;
-    int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-    const T* J = cr + CR_J;
-    for (int r = 0; r < 3; r++) {
-      T s = 0;
-      if (ta >= 0) {
-        int o = tree_dof(dm, ta);
-        for (int j = 0; j < nda; j++) s += J[r * CJ + j] * x[o + j];
-      }
-      if (tb >= 0) {
-        int o = tree_dof(dm, tb);
-        for (int j = 0; j < ndb; j++) s += J[r * CJ + nda + j] * x[o + j];
-      }
-      cr[CR_JA + r] = s;
+    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+    const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+    const T* J = cr + CR_J + r * CJ;
+    const T* Jb = J + nda;
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const T ja = J[j], xa = x[oa + j];
+      s += (j < nda ? ja : T(0)) * xa;
     }
-    T mu = cr[CR_MU], D = cr[CR_D];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const T jb = Jb[j], xb = x[ob + j];
+      s += (j < ndb ? jb : T(0)) * xb;
+    }
+    cr[slot + r] = s;
+  }
+}
+
+// constraint part of the primal cost at the current CR_JA / RR_JAR: sum of 1/2 D jar^2 over active rows
+template <typename T, typename DIM>
+__device__ __forceinline__ T rows_cost(const Ws<T, DIM>& w, int ncon, int nrow) {
+  T cst = 0;
+  for (int c = LANE; c < ncon; c += WAVE) {
+    const T* cr = w.cr() + CR_N * c;
+    const T mu = cr[CR_MU], D = cr[CR_D], bd = cr[CR_BD], kd = cr[CR_KD];
+#pragma unroll
     for (int e = 0; e < 4; e++) {
-      T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+      T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
       T jar = edge_val(cr + CR_JA, mu, e) - aref;
       if (jar < T(0)) cst += T(0.5) * D * jar * jar;
     }
   }
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
-    T* rr = w.rr() + RR_N * r;
-    T jar = rr[RR_C0] * x[ri[0]] + (ri[1] >= 0 ? rr[RR_C1] * x[ri[1]] : T(0)) - rr[RR_AREF];
-    rr[RR_JAR] = jar;
+    const T* rr = w.rr() + RR_N * r;
+    const T jar = rr[RR_JAR];
     if (ri[2] == 0 || jar < T(0)) cst += T(0.5) * rr[RR_D] * jar * jar;
   }
   return wave_sum(cst);
+}
+
+// evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
+template <typename T, typename DIM>
+__device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T, DIM>& w, const T* x, int ncon, int nrow) {
+  contact_jx(M, w, x, ncon, CR_JA);
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    T* rr = w.rr() + RR_N * r;
+    rr[RR_JAR] = rr[RR_C0] * x[ri[0]] + (ri[1] >= 0 ? rr[RR_C1] * x[ri[1]] : T(0)) - rr[RR_AREF];
+  }
+  SYNC();
+  return rows_cost(w, ncon, nrow);
 }
 
 // f3 (per contact, stored in CR_F[0..2]) = D * sum_active jar_e c_e ; used for gradient / forces
@@ -1963,17 +2087,21 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     for (int i = LANE; i < nv; i += WAVE) s += T(0.5) * tmp[i] * Ma[i];
     return wave_sum(s);
   };
-  // warmstart: the cheaper of qacc_warmstart and qacc_smooth
-  T c_ws = quad(a) + rows_eval(M, w, a, ncon, nrow);
+  // warmstart: the cheaper of qacc_warmstart and qacc_smooth.  The smooth candidate is evaluated first, so
+  // in the common case (the warmstart wins) the row products and M(a - as) left behind are already those
+  // of the chosen start and need no third evaluation
+  const T c_sm = quad(as) + rows_eval(M, w, as, ncon, nrow);
   SYNC();
-  T c_sm = quad(as) + rows_eval(M, w, as, ncon, nrow);
+  T qc = quad(a);
+  T cost = qc + rows_eval(M, w, a, ncon, nrow);
   SYNC();
-  if (!(c_ws < c_sm)) {
+  if (!(cost < c_sm)) {
     for (int i = LANE; i < nv; i += WAVE) a[i] = as[i];
+    SYNC();
+    qc = quad(a);
+    cost = qc + rows_eval(M, w, a, ncon, nrow);
+    SYNC();
   }
-  SYNC();
-  T cost = quad(a) + rows_eval(M, w, a, ncon, nrow);
-  SYNC();
   PMARK(PH_NSETUP);
   int it;
   const int maxit = M.solver_iter;
@@ -2146,24 +2274,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     PMARK(PH_NSOLVE);
     // exact line search along dir (segment walking over the breakpoints of the inequality rows)
     // Jd per contact (frame components) and per generic row
-    for (int c = LANE; c < ncon; c += WAVE) {
-      const int* ci = w.ci() + 4 * c;
-      T* cr = w.cr() + CR_N * c;
-      int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-      const T* J = cr + CR_J;
-      for (int r = 0; r < 3; r++) {
-        T s = 0;
-        if (ta >= 0) {
-          int o = tree_dof(dm, ta);
-          for (int j = 0; j < nda; j++) s += J[r * CJ + j] * dir[o + j];
-        }
-        if (tb >= 0) {
-          int o = tree_dof(dm, tb);
-          for (int j = 0; j < ndb; j++) s += J[r * CJ + nda + j] * dir[o + j];
-        }
-        cr[CR_JD + r] = s;
-      }
-    }
+    contact_jx(M, w, dir, ncon, CR_JD);
     for (int r = LANE; r < nrow; r += WAVE) {
       const int* ri = w.ri() + 4 * r;
       T* rr = w.rr() + RR_N * r;
@@ -2178,51 +2289,69 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     }
     dMd = wave_sum(dMd);
     dMa = wave_sum(dMa);
+    // the walk's per-row data is loop-invariant: one contact (4 pyramid edges) and one generic row per lane
+    // (ncon <= 64, nrow <= 64) held in registers; padding lanes carry jd = 0, D = 0 and contribute nothing
+    T ejar[4], ejd[4], ete[4], eD = T(0);
+    T gjar = T(0), gjd = T(0), gte = T(0), gD = T(0);
+    bool geq = false;
+    if (LANE < ncon) {
+      const T* cr = w.cr() + CR_N * LANE;
+      const T mu = cr[CR_MU], bd = cr[CR_BD], kd = cr[CR_KD];
+      eD = cr[CR_D];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
+        ejar[e] = edge_val(cr + CR_JA, mu, e) - aref;
+        ejd[e] = edge_val(cr + CR_JD, mu, e);
+        ete[e] = ejd[e] != T(0) ? -ejar[e] / ejd[e] : T(0);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        ejar[e] = T(1);
+        ejd[e] = T(0);
+        ete[e] = T(0);
+      }
+    }
+    if (LANE < nrow) {
+      const T* rr = w.rr() + RR_N * LANE;
+      geq = w.ri()[4 * LANE + 2] == 0;
+      gjar = rr[RR_JAR];
+      gjd = rr[RR_JD];
+      gD = rr[RR_D];
+      gte = gjd != T(0) ? -gjar / gjd : T(0);
+    }
     T alpha = 0;
     for (int ls = 0; ls < 4 * (4 * ncon + nrow) + 4; ls++) {
       T c0 = 0, c1 = 0, tn = T(3.0e38);
-      for (int c = LANE; c < ncon; c += WAVE) {
-        const T* cr = w.cr() + CR_N * c;
-        T mu = cr[CR_MU], D = cr[CR_D];
-        for (int e = 0; e < 4; e++) {
-          T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
-          T jar = edge_val(cr + CR_JA, mu, e) - aref;
-          T jd = edge_val(cr + CR_JD, mu, e);
-          bool act;
-          if (jd != T(0)) {
-            T te = -jar / jd;
-            if (jd < T(0)) {
-              act = te <= alpha;
-            } else {
-              act = alpha < te;
-            }
-            if (te > alpha && te < tn) tn = te;
-          } else {
-            act = jar < T(0);
-          }
-          if (act) {
-            c0 += D * (jar + alpha * jd) * jd;
-            c1 += D * jd * jd;
-          }
-        }
-      }
-      for (int r = LANE; r < nrow; r += WAVE) {
-        const int* ri = w.ri() + 4 * r;
-        const T* rr = w.rr() + RR_N * r;
-        T jar = rr[RR_JAR], jd = rr[RR_JD], D = rr[RR_D];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const T jar = ejar[e], jd = ejd[e], te = ete[e];
         bool act;
-        if (ri[2] == 0) {
-          act = true;
-        } else if (jd != T(0)) {
-          T te = -jar / jd;
+        if (jd != T(0)) {
           act = jd < T(0) ? te <= alpha : alpha < te;
           if (te > alpha && te < tn) tn = te;
         } else {
           act = jar < T(0);
         }
         if (act) {
-          c0 += D * (jar + alpha * jd) * jd;
-          c1 += D * jd * jd;
+          c0 += eD * (jar + alpha * jd) * jd;
+          c1 += eD * jd * jd;
+        }
+      }
+      {
+        bool act;
+        if (geq) {
+          act = true;
+        } else if (gjd != T(0)) {
+          act = gjd < T(0) ? gte <= alpha : alpha < gte;
+          if (gte > alpha && gte < tn) tn = gte;
+        } else {
+          act = gjar < T(0);
+        }
+        if (act) {
+          c0 += gD * (gjar + alpha * gjd) * gjd;
+          c1 += gD * gjd * gjd;
         }
       }
       c0 = wave_sum(c0) + dMa + alpha * dMd;
@@ -2236,9 +2365,23 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       }
       alpha = tn;
     }
-    for (int i = LANE; i < nv; i += WAVE) a[i] += alpha * dir[i];
+    // step: a, M (a - as) and the row products all move along dir (MuJoCo's Newton updates Jaref and Ma
+    // the same way instead of recomputing them); the quadratic part of the cost follows exactly
+    for (int i = LANE; i < nv; i += WAVE) {
+      a[i] += alpha * dir[i];
+      Ma[i] += alpha * tmp[i];
+    }
+    for (int e = LANE; e < 3 * ncon; e += WAVE) {
+      T* cr = w.cr() + CR_N * (e / 3) + e % 3;
+      cr[CR_JA] += alpha * cr[CR_JD];
+    }
+    for (int r = LANE; r < nrow; r += WAVE) {
+      T* rr = w.rr() + RR_N * r;
+      rr[RR_JAR] += alpha * rr[RR_JD];
+    }
     SYNC();
-    T newcost = quad(a) + rows_eval(M, w, a, ncon, nrow);
+    qc += alpha * dMa + T(0.5) * alpha * alpha * dMd;
+    T newcost = qc + rows_cost(w, ncon, nrow);
     SYNC();
     PMARK(PH_NLS);
     T improvement = scale * (cost - newcost);
@@ -2854,7 +2997,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
       if (LANE == 0) sc_[3] = __ballot(hit) != 0ull ? 1.0 : 0.0;
     }
     // gripper sites at the final state (the last mj_step1's site_xpos)
-    if (LANE < A) arm_chain(M, w, LANE, false);
+    if (LANE < A) arm_chain<T, DIM, false>(M, w, LANE);
     SYNC();
     // stage state for the next env-step = state before the TaskManager's teleports
     for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
