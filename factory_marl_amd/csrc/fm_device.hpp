@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -38,6 +39,16 @@
 #endif
 
 namespace fm {
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E) -- every index is a constant in the body
+// (a register array indexed through it stays in registers however large the body)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 #define LANE ((int)threadIdx.x)
 // A workgroup is exactly one wave, and a wave's LDS instructions execute in issue order, so LDS
@@ -1826,53 +1837,139 @@ __device__ __forceinline__ double readlane(double x, int l) {
 __device__ __forceinline__ float lane_bcast(float x, int l) { return readlane(x, l); }
 __device__ __forceinline__ double lane_bcast(double x, int l) { return __shfl(x, l); }
 
-// fp32 variant: the trailing-update operands L[i][k] are broadcast with v_readlane straight into SGPRs
-// (one VALU op each, no LDS round trip per pivot); the pivot itself is read the same way
-template <int NVM>
-__device__ __forceinline__ void chol_solve_rl(const float* H, int nv, const float* g, float* dir) {
-  const int j = LANE;
-  const float tiny = 1e-37f;
-  float col[NVM];
+template <typename T>
+__device__ __forceinline__ T edge_val(const T* x3, T mu, int e);
+
+// K_c = sum over the active pyramid edges e of D c_e c_e' (3x3 in contact-frame coordinates, edge directions
+// c_e = (1, +-mu, 0) / (1, 0, +-mu)), one contact per lane, stored 00 11 22 01 02 12 in CR_K
+template <typename T, typename DIM>
+__device__ __forceinline__ void contact_K(const Ws<T, DIM>& w, int ncon) {
+  for (int c = LANE; c < ncon; c += WAVE) {
+    T* cr = w.cr() + CR_N * c;
+    const T mu = cr[CR_MU], D = cr[CR_D], bd = cr[CR_BD], kd = cr[CR_KD];
+    T Kc[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < NVM; i++) col[i] = (i < nv && j < nv) ? H[i * nv + j] : 0.0f;
-  SYNC();
-  float dinv = 1.0f;
-#pragma unroll
-  for (int k = 0; k < NVM; k++) {
-    if (k < nv) {
-      float d = readlane(col[k], k);
-      d = d > tiny ? d : tiny;
-      const float ri = 1.0f / sqrtf(d);
-      const float lj = col[k] * ri;  // lane j >= k: L[j][k]
-      if (j == k) dinv = ri;
-      if (j >= k) col[k] = lj;
-      if (j > k) {
-#pragma unroll
-        for (int i = k + 1; i < NVM; i++)
-          if (i < nv) col[i] -= readlane(lj, i) * lj;
+    for (int e = 0; e < 4; e++) {
+      const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
+      const T jar = edge_val(cr + CR_JA, mu, e) - aref;
+      if (jar < T(0)) {
+        const T sg = (e & 1) ? -mu : mu;
+        Kc[0] += D;
+        if (e < 2) {
+          Kc[1] += D * sg * sg;
+          Kc[3] += D * sg;
+        } else {
+          Kc[2] += D * sg * sg;
+          Kc[4] += D * sg;
+        }
       }
     }
+#pragma unroll
+    for (int k = 0; k < 6; k++) cr[CR_K + k] = Kc[k];
   }
-  float acc = j < nv ? -g[j] : 0.0f;
+}
+
+__device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+
+// fp32, compile-time scene: Cholesky factor and solve of the Newton Hessian (assembled in LDS) for
+// dir = -H^-1 g, in registers (lane j owns column j; pivots and trailing operands broadcast by v_readlane).
+//  * Elimination order: cubes, arms, belt last (position p = dof - 1, the belt at NV - 1).  The belt touches
+//    every cube resting on it; eliminated last it is a border row instead of coupling all those cubes.
+//  * Tree-block sparsity: H couples two trees only through a contact between them.  The coupling graph (plus
+//    the fill-in of this elimination order) comes from the tree->contact masks; a pivot updates only the row
+//    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
+template <typename DIM>
+__device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<float, DIM>& w, const float* H,
+                                               const float* g, float* dir) {
+  constexpr int NV = DIM::nv, KK = DIM::K, AA = DIM::A, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
+  const int j = LANE;
+  const int jo = j == NV - 1 ? 0 : j + 1;  // lane j's dof (original numbering)
+  float col[NV];
+  // ---- H (assembled in LDS, row-major, original numbering) -> lane j holds column jo in elimination order
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    const int io = i == NV - 1 ? 0 : i + 1;
+    col[i] = j < NV ? H[io * NV + jo] : 0.0f;
+  }
+  SYNC();
+  // ---- tree coupling graph + fill-in of the elimination order (trees by rank: cubes, arms, belt)
+  unsigned adj[NT];
+  {
+    uint64_t tm[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const uint64_t m = w.tmask()[t];
+      tm[t] = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
+    }
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      unsigned a = 0;
+#pragma unroll
+      for (int u = 0; u < NT; u++)
+        if (u != t && (tm[t] & tm[u])) a |= 1u << u;
+      adj[t] = a;
+    }
+    auto rank = [](int t) { return t == 0 ? NT - 1 : t - 1; };
+#pragma unroll
+    for (int r = 0; r < NT; r++) {
+      const int t = r == NT - 1 ? 0 : r + 1;
+      unsigned later = 0;
+#pragma unroll
+      for (int u = 0; u < NT; u++)
+        if (rank(u) > r) later |= 1u << u;
+      const unsigned nb = adj[t] & later;
+#pragma unroll
+      for (int u = 0; u < NT; u++)
+        if (nb & (1u << u)) adj[u] |= nb & ~(1u << u);
+    }
+  }
+  // ---- factor (right-looking, pivots and trailing operands broadcast by v_readlane), coupled blocks only
+  const float tiny = 1e-37f;
+  float dinv = 1.0f;
+  static_for<0, NV>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int tk = k == NV - 1 ? 0 : (k < A0 - 1 ? 1 + k / 6 : 1 + KK + (k - (A0 - 1)) / 9);
+    float d = readlane(col[k], k);
+    d = d > tiny ? d : tiny;
+    const float ri = 1.0f / sqrtf(d);
+    const float lj = col[k] * ri;
+    if (j == k) dinv = ri;
+    if (j >= k) col[k] = lj;
+    const unsigned ak = adj[tk];
+    if (j > k) {
+      static_for<0, NT>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int ps = u == 0 ? NV - 1 : (u <= KK ? 6 * (u - 1) : A0 - 1 + 9 * (u - 1 - KK));
+        constexpr int pn = u == 0 ? 1 : (u <= KK ? 6 : 9);
+        if constexpr (ps + pn > k + 1) {                 // block not entirely at or above the pivot
+          if (u == tk || (ak & (1u << u))) {             // coupled to the pivot's tree
+#pragma unroll
+            for (int ii = 0; ii < pn; ii++) {
+              const int i = ps + ii;
+              if (i > k) col[i] -= readlane(lj, i) * lj;
+            }
+          }
+        }
+      });
+    }
+  });
+  float acc = j < NV ? -g[jo] : 0.0f;
   float y = 0.0f;
 #pragma unroll
-  for (int k = 0; k < NVM; k++) {
-    if (k < nv) {
-      const float yk = readlane(acc * dinv, k);
-      if (j == k) y = yk;
-      if (j > k) acc -= col[k] * yk;
-    }
+  for (int k = 0; k < NV; k++) {
+    const float yk = readlane(acc * dinv, k);
+    if (j == k) y = yk;
+    if (j > k) acc -= col[k] * yk;
   }
   float acc2 = y, x = 0.0f;
 #pragma unroll
-  for (int k = NVM - 1; k >= 0; k--) {
-    if (k < nv) {
-      const float xk = readlane(acc2 * dinv, k);
-      if (j == k) x = xk;
-      if (j < k) acc2 -= col[k] * dinv * xk;
-    }
+  for (int k = NV - 1; k >= 0; k--) {
+    const float xk = readlane(acc2 * dinv, k);
+    if (j == k) x = xk;
+    if (j < k) acc2 -= col[k] * dinv * xk;
   }
-  if (j < nv) dir[j] = x;
+  if (j < NV) dir[jo] = x;
   SYNC();
 }
 
@@ -2136,96 +2233,54 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     }
     SYNC();
     // contact blocks B_c' K_c B_c: K_c (3x3, from the active pyramid edges) for every contact at once, then
-    // all (contact, block entry) pairs in one pass accumulated with LDS atomics (one wave: deterministic)
-    {
-      int sz = 0;
-      if (LANE < ncon) {
-        T* cr = w.cr() + CR_N * LANE;
-        const int* ci = w.ci() + 4 * LANE;
-        T mu = cr[CR_MU], D = cr[CR_D];
-        T Kc[6] = {0, 0, 0, 0, 0, 0};  // 00 11 22 01 02 12
-        bool any = false;
-        for (int e = 0; e < 4; e++) {
-          T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
-          T jar = edge_val(cr + CR_JA, mu, e) - aref;
-          if (jar < T(0)) {
-            any = true;
-            T sg = (e & 1) ? -mu : mu;
-            Kc[0] += D;
-            if (e < 2) {
-              Kc[1] += D * sg * sg;
-              Kc[3] += D * sg;
-            } else {
-              Kc[2] += D * sg * sg;
-              Kc[4] += D * sg;
-            }
-          }
-        }
-        for (int k = 0; k < 6; k++) cr[CR_K + k] = Kc[k];
-        const int ncol = ((ci[3] >> 20) & 15) + ((ci[3] >> 24) & 15);
-        sz = any ? ncol * ncol : 0;
-      }
-      int incl = sz;
+    // one lane per (contact, block column ii) in fixed slots of CJ, adding its whole block column with LDS
+    // atomics (one wave: deterministic order)
+    contact_K(w, ncon);
+    SYNC();
+    for (int e = LANE; e < CJ * ncon; e += WAVE) {
+      const int c = e / CJ, ii = e - CJ * c;
+      const int* ci = w.ci() + 4 * c;
+      const T* cr = w.cr() + CR_N * c;
+      const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+      const int ncol = nda + ndb;
+      const T* Kc = cr + CR_K;
+      if (ii >= ncol || Kc[0] == T(0)) continue;
+      const T* J = cr + CR_J;
+      const T b0 = J[ii], b1 = J[CJ + ii], b2 = J[2 * CJ + ii];
+      const T q0 = Kc[0] * b0 + Kc[3] * b1 + Kc[4] * b2;
+      const T q1 = Kc[3] * b0 + Kc[1] * b1 + Kc[5] * b2;
+      const T q2 = Kc[4] * b0 + Kc[5] * b1 + Kc[2] * b2;
+      const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+      const int gi = ii < nda ? oa + ii : ob + ii - nda;
+      T* Hrow = H + gi * nv;
 #pragma unroll
-      for (int o = 1; o < WAVE; o <<= 1) {
-        int y = __shfl_up(incl, o);
-        if (LANE >= o) incl += y;
-      }
-      const int total = __shfl(incl, WAVE - 1);
-      int* hoff = w.misc() + 16;  // [64] exclusive block offsets (misc has room, see lds layout)
-      if (LANE < ncon) hoff[LANE] = incl - sz;
-      SYNC();
-      for (int e0 = 0; e0 < total; e0 += WAVE) {
-        const int e = e0 + LANE;
-        if (e < total) {
-          int lo = 0, hi = ncon - 1;
-          while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if (hoff[mid] <= e)
-              lo = mid;
-            else
-              hi = mid - 1;
-          }
-          const int* ci = w.ci() + 4 * lo;
-          const T* cr = w.cr() + CR_N * lo;
-          const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-          const int ncol = nda + ndb;
-          const int loc = e - hoff[lo];
-          const int ii = loc / ncol, jj = loc - ii * ncol;
-          const T* J = cr + CR_J;
-          const T* Kc = cr + CR_K;
-          T b0 = J[ii], b1 = J[CJ + ii], b2 = J[2 * CJ + ii];
-          T k0 = Kc[0] * J[jj] + Kc[3] * J[CJ + jj] + Kc[4] * J[2 * CJ + jj];
-          T k1 = Kc[3] * J[jj] + Kc[1] * J[CJ + jj] + Kc[5] * J[2 * CJ + jj];
-          T k2 = Kc[4] * J[jj] + Kc[5] * J[CJ + jj] + Kc[2] * J[2 * CJ + jj];
-          const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
-          const int gi = ii < nda ? oa + ii : ob + ii - nda;
+      for (int jj = 0; jj < CJ; jj++) {
+        if (jj < ncol) {
           const int gj = jj < nda ? oa + jj : ob + jj - nda;
-          atomicAdd(H + gi * nv + gj, b0 * k0 + b1 * k1 + b2 * k2);
+          atomicAdd(Hrow + gj, q0 * J[jj] + q1 * J[CJ + jj] + q2 * J[2 * CJ + jj]);
         }
       }
-      SYNC();
     }
-    if (LANE == 0) {
-      for (int r = 0; r < nrow; r++) {
-        const int* ri = w.ri() + 4 * r;
-        const T* rr = w.rr() + RR_N * r;
-        if (!(ri[2] == 0 || rr[RR_JAR] < T(0))) continue;
-        T D = rr[RR_D];
-        int d0 = ri[0], d1 = ri[1];
-        H[d0 * nv + d0] += D * rr[RR_C0] * rr[RR_C0];
-        if (d1 >= 0) {
-          H[d1 * nv + d1] += D * rr[RR_C1] * rr[RR_C1];
-          H[d0 * nv + d1] += D * rr[RR_C0] * rr[RR_C1];
-          H[d1 * nv + d0] += D * rr[RR_C0] * rr[RR_C1];
-        }
+    SYNC();
+    // generic rows, one per lane (rows may share a dof: atomics)
+    for (int r = LANE; r < nrow; r += WAVE) {
+      const int* ri = w.ri() + 4 * r;
+      const T* rr = w.rr() + RR_N * r;
+      if (!(ri[2] == 0 || rr[RR_JAR] < T(0))) continue;
+      const T D = rr[RR_D];
+      const int d0 = ri[0], d1 = ri[1];
+      atomicAdd(H + d0 * nv + d0, D * rr[RR_C0] * rr[RR_C0]);
+      if (d1 >= 0) {
+        atomicAdd(H + d1 * nv + d1, D * rr[RR_C1] * rr[RR_C1]);
+        atomicAdd(H + d0 * nv + d1, D * rr[RR_C0] * rr[RR_C1]);
+        atomicAdd(H + d1 * nv + d0, D * rr[RR_C0] * rr[RR_C1]);
       }
     }
     SYNC();
     PMARK(PH_NHESS);
     if (nv <= 48 && !(M.dbg_flags & 1)) {
       if constexpr (sizeof(T) == 4 && DIM::fixed)
-        chol_solve_rl<48>(H, nv, g, dir);
+        chol_sparse_rl<DIM>(M, w, H, g, dir);
       else
         chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
       PMARK(PH_NCHOL);
