@@ -297,6 +297,30 @@ __device__ __forceinline__ float wave_min(float x) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
 
+// inclusive prefix sum of an int over the wave on DPP (row shifts, then the row broadcasts; rocPRIM's
+// warp_scan_dpp sequence); full wave active at every call site
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  const int lane = (int)threadIdx.x, rl = lane & 15;
+  int t;
+  t = dpp_i32<0x111>(x);  // row_shr:1
+  if (rl >= 1) x += t;
+  t = dpp_i32<0x112>(x);  // row_shr:2
+  if (rl >= 2) x += t;
+  t = dpp_i32<0x114>(x);  // row_shr:4
+  if (rl >= 4) x += t;
+  t = dpp_i32<0x118>(x);  // row_shr:8
+  if (rl >= 8) x += t;
+  t = dpp_i32<0x142>(x);  // row_bcast:15
+  if ((lane & 31) >= 16) x += t;
+  t = dpp_i32<0x143>(x);  // row_bcast:31
+  if (lane >= 32) x += t;
+  return x;
+}
+
 template <typename T>
 struct StepParams {
   Model<T> M;

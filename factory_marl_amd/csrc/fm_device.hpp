@@ -1020,13 +1020,17 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   uint32_t* gs = w.gsurv();
   uint32_t* gsb = gs + 2 * WAVE;
   int nsurv = 0, nbb = 0;
+  // allowed body pairs are fetched one pass ahead (the global load overlaps the current pass)
+  uint32_t bpw_next = LANE < dm.ncbp ? M.cbp[LANE] : 0u;
   for (int p0 = 0; p0 < dm.ncbp; p0 += WAVE) {
     const int pidx = p0 + LANE;
     bool hit = false;
     int ncomb = 0;
     uint32_t bpw = 0;
+    const uint32_t bpw_cur = bpw_next;
+    bpw_next = pidx + WAVE < dm.ncbp ? M.cbp[pidx + WAVE] : 0u;
     if (pidx < dm.ncbp) {
-      bpw = M.cbp[pidx];
+      bpw = bpw_cur;
       const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
       const T* X = w.cbw() + 8 * b1;
       const T* Y = w.cbw() + 8 * b2;
@@ -1049,13 +1053,8 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     }
     const uint64_t bal = __ballot(hit);
     const int nsp = __popcll(bal);
-    int incl = ncomb;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-      int y = __shfl_up(incl, o);
-      if (LANE >= o) incl += y;
-    }
-    const int total = __shfl(incl, WAVE - 1);
+    const int incl = wave_incl_scan(ncomb);
+    const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
     if (hit) {
       int slot = __popcll(bal & below);
       sp[slot] = bpw;
@@ -1136,10 +1135,12 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   const int nst = misc[MISC_NSTAGE];
   const int ncon = nst < dm.maxcon ? nst : dm.maxcon;
   if (LANE == 0 && nst > dm.maxcon) ctr[0] += nst - dm.maxcon;
+  // rank of each staged contact among the staged keys (ncon <= 64: one per lane, keys broadcast by v_readlane)
+  const int mykey = LANE < ncon ? w.skey()[LANE] : 0x7fffffff;
+  int myrank = 0;
+  for (int t = 0; t < ncon; t++) myrank += __builtin_amdgcn_readlane(mykey, t) < mykey ? 1 : 0;
   for (int s = LANE; s < ncon; s += WAVE) {
-    const int key = w.skey()[s];
-    int rank = 0;
-    for (int t = 0; t < ncon; t++) rank += w.skey()[t] < key ? 1 : 0;
+    const int rank = myrank;
     const T* st = w.stage() + 8 * s;
     int* ci = w.ci() + 4 * rank;
     T* cr = w.cr() + CR_N * rank;
