@@ -956,7 +956,9 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   const int* cbi = w.cbi();
   int* misc = w.misc();
   const uint64_t below = (1ull << LANE) - 1ull;
-  // 1. geom centres + rbound (the buffer is phase-local, so static geoms are rewritten too)
+  // 1. geom centres + rbound (the buffer is phase-local, so static geoms are rewritten too); unrolled so the
+  // scene-table loads of every pass issue together
+#pragma unroll
   for (int g = LANE; g < dm.ngc; g += WAVE) {
     const int kb = (gin[g] >> 8) & 255;
     const T* gg = M.geom + 16 * g;
@@ -987,6 +989,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     }
   }
   // 2. collision-body bounds
+#pragma unroll
   for (int b = LANE; b < dm.ncb; b += WAVE) {
     const int kb = cbi[4 * b], fl = cbi[4 * b + 1];
     T* o = w.cbw() + 8 * b;
@@ -1591,32 +1594,48 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     int kb1 = (gi1 >> 8) & 255, kb2 = (gi2 >> 8) & 255;
     int tr1 = kbody_tree(dm, kb1), tr2 = kbody_tree(dm, kb2);
     int armflag = ((gi1 | gi2) >> GI_ARM) & 1;
-    // frame (mju_makeFrame)
-    T* f = cr + CR_FR;
-    T nn = sqrt(dot3(f, f));
-    if (nn < T(1e-15)) {
-      f[0] = 1;
-      f[1] = f[2] = 0;
-    } else {
-      f[0] /= nn;
-      f[1] /= nn;
-      f[2] /= nn;
+    // frame (mju_makeFrame), built in registers and stored once
+    T f[9];
+    {
+      T* fs = cr + CR_FR;
+      T n0 = fs[0], n1 = fs[1], n2 = fs[2];
+      const T nn = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+      if (nn < T(1e-15)) {
+        n0 = 1;
+        n1 = n2 = 0;
+      } else {
+        n0 /= nn;
+        n1 /= nn;
+        n2 /= nn;
+      }
+      T t0 = 0, t1 = 0, t2 = 0;
+      if (n1 < T(0.5) && n1 > T(-0.5))
+        t1 = 1;
+      else
+        t2 = 1;
+      const T tt = n0 * t0 + n1 * t1 + n2 * t2;
+      t0 -= tt * n0;
+      t1 -= tt * n1;
+      t2 -= tt * n2;
+      const T m = sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+      if (m < T(1e-15)) {
+        t0 = 1;
+        t1 = t2 = 0;
+      } else {
+        t0 /= m;
+        t1 /= m;
+        t2 /= m;
+      }
+      f[0] = n0;
+      f[1] = n1;
+      f[2] = n2;
+      f[3] = t0;
+      f[4] = t1;
+      f[5] = t2;
+      cross3(f, f + 3, f + 6);
+#pragma unroll
+      for (int k = 0; k < 9; k++) fs[k] = f[k];
     }
-    f[3] = f[4] = f[5] = 0;
-    if (f[1] < T(0.5) && f[1] > T(-0.5))
-      f[4] = 1;
-    else
-      f[5] = 1;
-    T tt = dot3(f, f + 3);
-    for (int k = 0; k < 3; k++) f[3 + k] -= tt * f[k];
-    T n2 = sqrt(dot3(f + 3, f + 3));
-    if (n2 < T(1e-15)) {
-      f[3] = 1;
-      f[4] = f[5] = 0;
-    } else {
-      for (int k = 0; k < 3; k++) f[3 + k] /= n2;
-    }
-    cross3(f, f + 3, f + 6);
     // Jacobian blocks B = frame * (J(body2) - J(body1)) on the contact point
     int ta = -1, tb = -1;
     if (tr1 >= 0) ta = tr1;
@@ -1628,7 +1647,7 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     }
     int nda = ta >= 0 ? tree_nd(dm, ta) : 0;
     int ndb = tb >= 0 ? tree_nd(dm, tb) : 0;
-    const T* p = cr + CR_POS;
+    const T p[3] = {cr[CR_POS], cr[CR_POS + 1], cr[CR_POS + 2]};
     T* J = cr + CR_J;
     for (int blk = 0; blk < 2; blk++) {
       int t = blk == 0 ? ta : tb;
