@@ -22,20 +22,18 @@ def _have_gpu():
     return torch.cuda.is_available()
 
 
-@pytest.fixture(scope="module")
-def trajectory(oracle):
+def _rollout(oracle, A_, K_, T, reward="progress", seed_actions=7):
     """oracle rollout: states before each step, actions, and the post-step results"""
     from factory_marl_amd import state as st
 
-    rng = np.random.default_rng(7)
-    e = oracle.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4))
+    rng = np.random.default_rng(seed_actions)
+    e = oracle.Env(A_, K_, 42, reward=reward, weights=(0.2, 0.4, 0.1, 0.4))
     e.reset()
     recs, acts, outs = [], [], []
-    T = 96
     for t in range(T):
         d, i, r = e.export_state()
-        recs.append(st.pack(A, K, d, i, r))
-        a = rng.uniform(-2, 2, 8 * A).astype(np.float32)
+        recs.append(st.pack(A_, K_, d, i, r))
+        a = rng.uniform(-2, 2, 8 * A_).astype(np.float32)
         obs, rew, term, _, info = e.step(a)
         d2, i2, r2 = e.export_state()
         outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
@@ -45,23 +43,29 @@ def trajectory(oracle):
     return np.stack(recs), np.stack(acts), outs
 
 
-def _gpu_env(n, precision):
+@pytest.fixture(scope="module")
+def trajectory(oracle):
+    return _rollout(oracle, A, K, 96)
+
+
+def _gpu_env(n, precision, A_=A, K_=K, env_class="AllFullRLProgressRewardEnv"):
     from factory_marl_amd import FactoryVecEnv
 
-    kw = dict(num_arms=A, max_num_objects=K, seed=42, small_action_norm_reward_factor=0.1)
-    env = FactoryVecEnv(n, env_kwargs=kw, precision=precision)
+    kw = dict(num_arms=A_, max_num_objects=K_, seed=42, small_action_norm_reward_factor=0.1)
+    env = FactoryVecEnv(n, env_class=env_class, env_kwargs=kw, precision=precision)
     env.reset()
     return env
 
 
-def _compare(trajectory, precision, tol_rel):
+def _compare(trajectory, precision, tol_rel, A_=A, K_=K, env_class="AllFullRLProgressRewardEnv"):
     """returns per-step relative state errors (SURVEY metric), and the steps whose integer task state,
     flags, obs or reward disagree"""
     from factory_marl_amd import state as st
 
+    A, K = A_, K_
     recs, acts, outs = trajectory
     n = len(recs)
-    env = _gpu_env(n, precision)
+    env = _gpu_env(n, precision, A, K, env_class)
     env.set_state(recs)
     obs, rew, term, trunc = env.step_tensors(torch.as_tensor(acts, device=env.device))
     env.sync()
@@ -179,8 +183,12 @@ def test_full_size_properties():
     assert np.isfinite(d).all()
     q = d[:, :nq]
     for k in range(K):
-        qn = np.linalg.norm(q[:, 1 + 7 * k + 3:1 + 7 * k + 7], axis=1)
-        assert np.all(np.abs(qn - 1) < 1e-4) or True  # spawn quaternions are unnormalised until integrated
+        # unit quaternions, except a cube spawned by this env-step's TaskManager (pose (0, 1, 2) with the raw
+        # U(0,1)^4 draw, task_utils.py:47-52) -- it is normalised on use and by its first integration
+        qk = q[:, 1 + 7 * k:1 + 7 * k + 7]
+        spawned = np.all(qk[:, :3] == [0.0, 1.0, 2.0], axis=1)
+        qn = np.linalg.norm(qk[:, 3:], axis=1)
+        assert np.all(np.abs(qn[~spawned] - 1) < 1e-4)
     assert env.counters()[:, 0].sum() == 0
     env.close()
     env2 = _gpu_env(n, "fp32")
@@ -189,3 +197,62 @@ def test_full_size_properties():
     env2.sync()
     assert torch.equal(obs1, env2.obs), "kernel is not deterministic"
     env2.close()
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("A_,K_,env_class,reward", [
+    (2, 8, "AllFullRLProgressRewardEnv", "progress"),   # compile-time scene FixedDims<2, 8>
+    (2, 6, "AllFullRLProgressRewardEnv", "progress"),   # runtime-dims kernel (no specialisation for K = 6)
+    (2, 4, "AllFullRLScoreEnv", "score"),               # score-delta reward (environments.py:129-149)
+])
+def test_teacher_forced_fp64_other_configs(oracle, A_, K_, env_class, reward):
+    """same gate as the (2, 4) benchmark scene: fp64 within 1e-7 per env-step, integer state / flags exact"""
+    traj = _rollout(oracle, A_, K_, 40, reward=reward, seed_actions=3)
+    r = _compare(traj, "fp64", 1e-7, A_, K_, env_class)
+    print(f"fp64 ({A_},{K_}) {env_class}: worst rel err {r['errs'].max():.3e}, obs {r['obs_err'].max():.2e}")
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    assert r["errs"].max() <= 1e-7
+    assert r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
+    assert r["counters"][:, 0].sum() == 0
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_fp32_other_scene_within_survey_gate(oracle):
+    """fp32 (2, 8) compile-time scene: integer state / flags exact, SURVEY gate on most env-steps"""
+    traj = _rollout(oracle, 2, 8, 48, seed_actions=5)
+    r = _compare(traj, "fp32", 1e-4, 2, 8)
+    frac = float(np.mean(r["errs"] <= 1e-4))
+    print(f"fp32 (2,8): {frac:.1%} of {len(r['errs'])} steps within 1e-4; median {np.median(r['errs']):.2e}")
+    assert not r["flag_bad"] and len(r["int_bad"]) == 0
+    # measured 79 % on this 48-step trajectory (the (2, 4) scene: 90 %): more cubes, more contact events that
+    # flip under fp32 rounding inside the 100 substeps; the fp64 build holds 1e-7 on every step of it
+    assert frac >= 0.75
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_masked_reset_only_touches_masked_arenas():
+    """fm_reset with a mask (env_method("reset", indices=...)): other arenas keep their state bit for bit"""
+    env = _gpu_env(8, "fp32")
+    g = torch.Generator(device=env.device)
+    g.manual_seed(1)
+    for _ in range(3):
+        env.step_tensors(torch.rand(8, 8 * A, device=env.device, generator=g) * 2 - 1)
+    env.sync()
+    before = env.get_state()
+    mask = np.zeros(8, np.uint8)
+    mask[[1, 5]] = 1
+    env.reset(mask=mask)
+    env.sync()
+    after = env.get_state()
+    fresh = _gpu_env(1, "fp32").get_state()[0]
+    for i in range(8):
+        if mask[i]:
+            from factory_marl_amd import state as st
+
+            da, ia, _ = st.unpack(A, K, after[i])
+            df, i_f, _ = st.unpack(A, K, fresh)
+            nq = st.sizes(A, K)[0]
+            assert np.array_equal(da[:nq], df[:nq])  # reset pose
+        else:
+            assert np.array_equal(after[i], before[i])
+    env.close()
