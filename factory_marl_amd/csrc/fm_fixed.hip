@@ -1,10 +1,17 @@
 // fm_fixed.hip -- one compile-time scene (FM_A arms, FM_K objects): instantiates the env-step kernel
-// with FixedDims<FM_A, FM_K> (constexpr dims and LDS layout) for fp32 and fp64.  Built once per scene by
-// the Makefile (fm_fixed_<A>_<K>.o) so the scenes compile in parallel.
+// with FixedDims<FM_A, FM_K> (constexpr dims and LDS layout) for one precision (FM_PREC 32 or 64).  Built
+// once per scene and precision by the Makefile (fm_fixed_<A>_<K>_f<P>.o) so they compile in parallel.
 #include "fm_device.hpp"
 
 #ifndef FM_A
-#error "compile with -DFM_A=<arms> -DFM_K=<objects>"
+#error "compile with -DFM_A=<arms> -DFM_K=<objects> -DFM_PREC=<32|64>"
+#endif
+#if FM_PREC == 32
+#define FM_REAL float
+#elif FM_PREC == 64
+#define FM_REAL double
+#else
+#error "FM_PREC must be 32 or 64"
 #endif
 
 namespace fm {
@@ -20,9 +27,7 @@ void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStre
   hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
 }
 
-template hipError_t fixed_set_attr<float, FM_A, FM_K>(int);
-template hipError_t fixed_set_attr<double, FM_A, FM_K>(int);
-template void fixed_launch<float, FM_A, FM_K>(const StepParams<float>&, int, int, hipStream_t);
-template void fixed_launch<double, FM_A, FM_K>(const StepParams<double>&, int, int, hipStream_t);
+template hipError_t fixed_set_attr<FM_REAL, FM_A, FM_K>(int);
+template void fixed_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, int, hipStream_t);
 
 }  // namespace fm
