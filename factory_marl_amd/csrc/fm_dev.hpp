@@ -167,7 +167,7 @@ struct Lay {
   int Marm;
   int gx;     // T [ngc][4]  geom world centre, rbound
   int ginfo, cbi, cbw, cbg;  // LDS copies of the geom / collision-body tables, body bounds T [ncb][8]
-  int sp, spoff, gsurv;      // broadphase work lists
+  int sp, gsurv;             // broadphase work lists
   int stage, skey, spw;      // staged contacts T [maxcon][8], keys, pair words
   int cube;                  // T [K][4] this arena's cube h, m, I
   int H;
@@ -384,8 +384,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   off = u0;
   L.gx = take(tsize * 4 * ngc);
   L.cbw = take(tsize * 8 * ncb);
-  L.sp = take(4 * WAVE);
-  L.spoff = take(4 * WAVE);
+  L.sp = take(4 * (ncb * (ncb - 1) / 2));  // every possible body pair can pass the midphase
   L.gsurv = take(4 * 4 * WAVE);
   L.stage = take(tsize * 8 * maxcon);
   L.skey = take(4 * maxcon);

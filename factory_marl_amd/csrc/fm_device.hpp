@@ -326,14 +326,6 @@ struct Ws {
       return (uint32_t*)(base + L->sp);
     }
   }
-  __device__ __forceinline__ int* spoff() const {
-    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
-      constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (int*)(base + c.spoff);
-    } else {
-      return (int*)(base + L->spoff);
-    }
-  }
   __device__ __forceinline__ uint32_t* gsurv() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -1015,121 +1007,122 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   }
   if (LANE == 0) misc[MISC_NSTAGE] = 0;
   SYNC();
+  // 3. midphase: every allowed body pair's bounding test; the hits are compacted into sp[] (body pair | first
+  // geom-pair index << 16) in one sweep, so the geom-pair expansion below runs over all of them at once
   uint32_t* sp = w.sp();
-  int* spoff = w.spoff();
-  // survivors are binned by narrowphase cost: box-box pairs (SAT + face clipping) in gsb, everything else
-  // (sphere-box, sphere-sphere, plane-*) in gs, so a batch of 64 lanes runs one code path instead of the
-  // union of all of them
+  int nsp = 0, total = 0;
+  {
+    // allowed body pairs are fetched one pass ahead (the global load overlaps the current pass)
+    uint32_t bpw_next = LANE < dm.ncbp ? M.cbp[LANE] : 0u;
+    for (int p0 = 0; p0 < dm.ncbp; p0 += WAVE) {
+      const int pidx = p0 + LANE;
+      bool hit = false;
+      int ncomb = 0;
+      const uint32_t bpw = bpw_next;
+      bpw_next = pidx + WAVE < dm.ncbp ? M.cbp[pidx + WAVE] : 0u;
+      if (pidx < dm.ncbp) {
+        const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
+        const T* X = w.cbw() + 8 * b1;
+        const T* Y = w.cbw() + 8 * b2;
+        const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1];
+        if (f1 & CB_PLANE) {
+          hit = Y[2] - Y[6] - Y[3] <= T(0);
+        } else if (f2 & CB_PLANE) {
+          hit = X[2] - X[6] - X[3] <= T(0);
+        } else {
+          T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
+          T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
+          T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
+          d0 = d0 > T(0) ? d0 : T(0);
+          d1 = d1 > T(0) ? d1 : T(0);
+          d2 = d2 > T(0) ? d2 : T(0);
+          T rr = X[3] + Y[3];
+          hit = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
+        }
+        if (hit) ncomb = cbi[4 * b1 + 3] * cbi[4 * b2 + 3];
+      }
+      const uint64_t bal = __ballot(hit);
+      const int incl = wave_incl_scan(ncomb);
+      if (hit) sp[nsp + __popcll(bal & below)] = (bpw & 0xFFFFu) | ((uint32_t)(total + incl - ncomb) << 16);
+      nsp += __popcll(bal);
+      total += __builtin_amdgcn_readlane(incl, WAVE - 1);
+    }
+  }
+  // pair-class -> params table, one entry per lane (read back with ds_bpermute, no memory access)
+  const int ptab_l = LANE < 25 ? M.ptab[LANE] : 0;
+  SYNC();
+  // 4. geom pairs of the hit body pairs, 64 per pass: bounding-sphere test, then binned by narrowphase cost:
+  // box-box pairs (SAT + face clipping) in gsb, everything else (sphere-box, sphere-sphere, plane-*) in gs,
+  // so a batch of 64 lanes runs one code path instead of the union of all of them
   uint32_t* gs = w.gsurv();
   uint32_t* gsb = gs + 2 * WAVE;
   int nsurv = 0, nbb = 0;
-  // allowed body pairs are fetched one pass ahead (the global load overlaps the current pass)
-  uint32_t bpw_next = LANE < dm.ncbp ? M.cbp[LANE] : 0u;
-  for (int p0 = 0; p0 < dm.ncbp; p0 += WAVE) {
-    const int pidx = p0 + LANE;
-    bool hit = false;
-    int ncomb = 0;
-    uint32_t bpw = 0;
-    const uint32_t bpw_cur = bpw_next;
-    bpw_next = pidx + WAVE < dm.ncbp ? M.cbp[pidx + WAVE] : 0u;
-    if (pidx < dm.ncbp) {
-      bpw = bpw_cur;
-      const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
-      const T* X = w.cbw() + 8 * b1;
-      const T* Y = w.cbw() + 8 * b2;
-      const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1];
-      if (f1 & CB_PLANE) {
-        hit = Y[2] - Y[6] - Y[3] <= T(0);
-      } else if (f2 & CB_PLANE) {
-        hit = X[2] - X[6] - X[3] <= T(0);
-      } else {
-        T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
-        T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
-        T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
-        d0 = d0 > T(0) ? d0 : T(0);
-        d1 = d1 > T(0) ? d1 : T(0);
-        d2 = d2 > T(0) ? d2 : T(0);
-        T rr = X[3] + Y[3];
-        hit = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
+  for (int e0 = 0; e0 < total; e0 += WAVE) {
+    const int e = e0 + LANE;
+    bool ok = false;
+    uint32_t pk = 0;
+    int pc = 0;
+    if (e < total) {
+      int lo = 0, hi = nsp - 1;
+      while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if ((int)(sp[mid] >> 16) <= e)
+          lo = mid;
+        else
+          hi = mid - 1;
       }
-      if (hit) ncomb = cbi[4 * b1 + 3] * cbi[4 * b2 + 3];
+      const uint32_t bp = sp[lo];
+      const int x = bp & 255, y = (bp >> 8) & 255;
+      const int r = e - (int)(bp >> 16);
+      const int ngy = cbi[4 * y + 3];
+      const int i = r / ngy, j = r - i * ngy;
+      int ga = w.cbg()[cbi[4 * x + 2] + i], gb = w.cbg()[cbi[4 * y + 2] + j];
+      const T* xa = gx + 4 * ga;
+      const T* xb = gx + 4 * gb;
+      ok = true;
+      if (xa[3] > T(0) && xb[3] > T(0)) {
+        T d0 = xa[0] - xb[0], d1 = xa[1] - xb[1], d2 = xa[2] - xb[2];
+        T rs = xa[3] + xb[3];
+        ok = sqrt(d0 * d0 + d1 * d1 + d2 * d2) <= rs;
+      }
+      if (ok) {
+        int c1 = ga < gb ? ga : gb, c2 = ga < gb ? gb : ga;
+        if ((gin[c1] & 3) > (gin[c2] & 3)) {
+          int t = c1;
+          c1 = c2;
+          c2 = t;
+        }
+        pc = 5 * ((gin[c1] >> GI_PC) & 7) + ((gin[c2] >> GI_PC) & 7);
+        pk = (uint32_t)c1 | ((uint32_t)c2 << 12);
+      }
     }
-    const uint64_t bal = __ballot(hit);
-    const int nsp = __popcll(bal);
-    const int incl = wave_incl_scan(ncomb);
-    const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
-    if (hit) {
-      int slot = __popcll(bal & below);
-      sp[slot] = bpw;
-      spoff[slot] = incl - ncomb;
-    }
+    pk |= (uint32_t)__builtin_amdgcn_ds_bpermute(pc << 2, ptab_l) << 24;
+    const bool isbb = ok && (gin[pk & 4095] & 3) == GC_BOX;  // type-ordered: c1 box => both boxes
+    const uint64_t b2m = __ballot(ok && !isbb);
+    const uint64_t bbm = __ballot(isbb);
+    if (ok && !isbb) gs[nsurv + __popcll(b2m & below)] = pk;
+    if (isbb) gsb[nbb + __popcll(bbm & below)] = pk;
+    nsurv += __popcll(b2m);
+    nbb += __popcll(bbm);
     SYNC();
-    for (int e0 = 0; e0 < total; e0 += WAVE) {
-      const int e = e0 + LANE;
-      bool ok = false;
-      uint32_t pk = 0;
-      if (e < total) {
-        int lo = 0, hi = nsp - 1;
-        while (lo < hi) {
-          int mid = (lo + hi + 1) >> 1;
-          if (spoff[mid] <= e)
-            lo = mid;
-          else
-            hi = mid - 1;
-        }
-        const uint32_t bp = sp[lo];
-        const int x = bp & 255, y = (bp >> 8) & 255;
-        const int r = e - spoff[lo];
-        const int ngy = cbi[4 * y + 3];
-        const int i = r / ngy, j = r - i * ngy;
-        int ga = w.cbg()[cbi[4 * x + 2] + i], gb = w.cbg()[cbi[4 * y + 2] + j];
-        const T* xa = gx + 4 * ga;
-        const T* xb = gx + 4 * gb;
-        ok = true;
-        if (xa[3] > T(0) && xb[3] > T(0)) {
-          T d0 = xa[0] - xb[0], d1 = xa[1] - xb[1], d2 = xa[2] - xb[2];
-          T rs = xa[3] + xb[3];
-          ok = sqrt(d0 * d0 + d1 * d1 + d2 * d2) <= rs;
-        }
-        if (ok) {
-          int c1 = ga < gb ? ga : gb, c2 = ga < gb ? gb : ga;
-          if ((gin[c1] & 3) > (gin[c2] & 3)) {
-            int t = c1;
-            c1 = c2;
-            c2 = t;
-          }
-          int pc = 5 * ((gin[c1] >> GI_PC) & 7) + ((gin[c2] >> GI_PC) & 7);
-          pk = (uint32_t)c1 | ((uint32_t)c2 << 12) | ((uint32_t)M.ptab[pc] << 24);
-        }
-      }
-      const bool isbb = ok && (gin[pk & 4095] & 3) == GC_BOX;  // type-ordered: c1 box => both boxes
-      const uint64_t b2m = __ballot(ok && !isbb);
-      const uint64_t bbm = __ballot(isbb);
-      if (ok && !isbb) gs[nsurv + __popcll(b2m & below)] = pk;
-      if (isbb) gsb[nbb + __popcll(bbm & below)] = pk;
-      nsurv += __popcll(b2m);
-      nbb += __popcll(bbm);
+    if (nsurv >= WAVE) {
+      narrow_batch(M, w, gs, WAVE);
+      const bool mv = LANE + WAVE < nsurv;
+      uint32_t t = mv ? gs[LANE + WAVE] : 0u;
       SYNC();
-      if (nsurv >= WAVE) {
-        narrow_batch(M, w, gs, WAVE);
-        const bool mv = LANE + WAVE < nsurv;
-        uint32_t t = mv ? gs[LANE + WAVE] : 0u;
-        SYNC();
-        if (mv) gs[LANE] = t;
-        nsurv -= WAVE;
-        SYNC();
-      }
-      if (nbb >= WAVE) {
-        narrow_batch(M, w, gsb, WAVE);
-        const bool mv = LANE + WAVE < nbb;
-        uint32_t t = mv ? gsb[LANE + WAVE] : 0u;
-        SYNC();
-        if (mv) gsb[LANE] = t;
-        nbb -= WAVE;
-        SYNC();
-      }
+      if (mv) gs[LANE] = t;
+      nsurv -= WAVE;
+      SYNC();
     }
-    SYNC();
+    if (nbb >= WAVE) {
+      narrow_batch(M, w, gsb, WAVE);
+      const bool mv = LANE + WAVE < nbb;
+      uint32_t t = mv ? gsb[LANE + WAVE] : 0u;
+      SYNC();
+      if (mv) gsb[LANE] = t;
+      nbb -= WAVE;
+      SYNC();
+    }
   }
   if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
   if (nbb > 0) narrow_batch(M, w, gsb, nbb);

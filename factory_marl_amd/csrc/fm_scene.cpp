@@ -520,7 +520,8 @@ bool build_scene(int A, int K, int N, const uint64_t* seeds, SceneHost& s, std::
       }
       s.pairs.push_back((uint32_t)c1 | ((uint32_t)c2 << 12) | ((uint32_t)pi << 24));
     }
-  if (ng >= 4096 || s.params.size() > 255) {
+  // (geom-pair indices of one broadphase sweep are kept in 16 bits)
+  if (ng >= 4096 || s.params.size() > 255 || s.pairs.size() >= 65536) {
     err = "scene too large for the pair encoding";
     return false;
   }
