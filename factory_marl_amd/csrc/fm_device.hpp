@@ -938,6 +938,15 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
   }
 }
 
+// midphase passes of 64 body pairs that cover every possible pair of a compile-time scene
+template <typename DIM>
+__device__ constexpr int body_pair_passes() {
+  if constexpr (DIM::fixed)
+    return (DIM::ncb * (DIM::ncb - 1) / 2 + WAVE - 1) / WAVE;
+  else
+    return 1;
+}
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
   const DIM dm(M.dm);
@@ -948,6 +957,14 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   const int* cbi = w.cbi();
   int* misc = w.misc();
   const uint64_t below = (1ull << LANE) - 1ull;
+  // compile-time scene: the allowed body pairs (a scene constant in global memory) are all requested up front,
+  // so their latency hides behind the geom / bound passes
+  constexpr int NPP = body_pair_passes<DIM>();
+  uint32_t bpr[NPP];
+  if constexpr (DIM::fixed) {
+#pragma unroll
+    for (int k = 0; k < NPP; k++) bpr[k] = k * WAVE + LANE < dm.ncbp ? M.cbp[k * WAVE + LANE] : 0u;
+  }
   // 1. geom centres + rbound (the buffer is phase-local, so static geoms are rewritten too); unrolled so the
   // scene-table loads of every pass issue together
 #pragma unroll
@@ -1011,41 +1028,47 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // geom-pair index << 16) in one sweep, so the geom-pair expansion below runs over all of them at once
   uint32_t* sp = w.sp();
   int nsp = 0, total = 0;
-  {
+  auto sweep = [&](uint32_t bpw, int pidx) {
+    bool hit = false;
+    int ncomb = 0;
+    if (pidx < dm.ncbp) {
+      const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
+      const T* X = w.cbw() + 8 * b1;
+      const T* Y = w.cbw() + 8 * b2;
+      const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1];
+      if (f1 & CB_PLANE) {
+        hit = Y[2] - Y[6] - Y[3] <= T(0);
+      } else if (f2 & CB_PLANE) {
+        hit = X[2] - X[6] - X[3] <= T(0);
+      } else {
+        T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
+        T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
+        T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
+        d0 = d0 > T(0) ? d0 : T(0);
+        d1 = d1 > T(0) ? d1 : T(0);
+        d2 = d2 > T(0) ? d2 : T(0);
+        T rr = X[3] + Y[3];
+        hit = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
+      }
+      if (hit) ncomb = cbi[4 * b1 + 3] * cbi[4 * b2 + 3];
+    }
+    const uint64_t bal = __ballot(hit);
+    const int incl = wave_incl_scan(ncomb);
+    if (hit) sp[nsp + __popcll(bal & below)] = (bpw & 0xFFFFu) | ((uint32_t)(total + incl - ncomb) << 16);
+    nsp += __popcll(bal);
+    total += __builtin_amdgcn_readlane(incl, WAVE - 1);
+  };
+  if constexpr (DIM::fixed) {
+#pragma unroll
+    for (int k = 0; k < NPP; k++)
+      if (k * WAVE < dm.ncbp) sweep(bpr[k], k * WAVE + LANE);
+  } else {
     // allowed body pairs are fetched one pass ahead (the global load overlaps the current pass)
     uint32_t bpw_next = LANE < dm.ncbp ? M.cbp[LANE] : 0u;
     for (int p0 = 0; p0 < dm.ncbp; p0 += WAVE) {
-      const int pidx = p0 + LANE;
-      bool hit = false;
-      int ncomb = 0;
       const uint32_t bpw = bpw_next;
-      bpw_next = pidx + WAVE < dm.ncbp ? M.cbp[pidx + WAVE] : 0u;
-      if (pidx < dm.ncbp) {
-        const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
-        const T* X = w.cbw() + 8 * b1;
-        const T* Y = w.cbw() + 8 * b2;
-        const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1];
-        if (f1 & CB_PLANE) {
-          hit = Y[2] - Y[6] - Y[3] <= T(0);
-        } else if (f2 & CB_PLANE) {
-          hit = X[2] - X[6] - X[3] <= T(0);
-        } else {
-          T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
-          T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
-          T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
-          d0 = d0 > T(0) ? d0 : T(0);
-          d1 = d1 > T(0) ? d1 : T(0);
-          d2 = d2 > T(0) ? d2 : T(0);
-          T rr = X[3] + Y[3];
-          hit = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
-        }
-        if (hit) ncomb = cbi[4 * b1 + 3] * cbi[4 * b2 + 3];
-      }
-      const uint64_t bal = __ballot(hit);
-      const int incl = wave_incl_scan(ncomb);
-      if (hit) sp[nsp + __popcll(bal & below)] = (bpw & 0xFFFFu) | ((uint32_t)(total + incl - ncomb) << 16);
-      nsp += __popcll(bal);
-      total += __builtin_amdgcn_readlane(incl, WAVE - 1);
+      bpw_next = p0 + WAVE + LANE < dm.ncbp ? M.cbp[p0 + WAVE + LANE] : 0u;
+      sweep(bpw, p0 + LANE);
     }
   }
   // pair-class -> params table, one entry per lane (read back with ds_bpermute, no memory access)
