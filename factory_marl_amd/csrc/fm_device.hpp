@@ -1980,10 +1980,15 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<f
         constexpr int pn = u == 0 ? 1 : (u <= KK ? 6 : 9);
         if constexpr (ps + pn > k + 1) {                 // block not entirely at or above the pivot
           if (u == tk || (ak & (1u << u))) {             // coupled to the pivot's tree
+            // the block's operands are broadcast first, then used: the v_readlane -> VALU hazard is paid once
+            // per block instead of once per entry
+            float lv[pn];
+#pragma unroll
+            for (int ii = 0; ii < pn; ii++) lv[ii] = ps + ii > k ? readlane(lj, ps + ii) : 0.0f;
 #pragma unroll
             for (int ii = 0; ii < pn; ii++) {
               const int i = ps + ii;
-              if (i > k) col[i] -= readlane(lj, i) * lj;
+              if (i > k) col[i] -= lv[ii] * lj;
             }
           }
         }
