@@ -185,8 +185,9 @@ struct Lay {
   int total;
 };
 
-// per-contact real record
-enum { CR_DIST = 0, CR_MU, CR_D, CR_KD, CR_BD, CR_POS, CR_FR = CR_POS + 3, CR_J = CR_FR + 9, CR_VEL = CR_J + 3 * CJ,
+// per-contact real record; the Jacobian block first, so its three rows of CJ (even) start 8-byte aligned
+// (records are CR_N = 84 reals, a multiple of 16 bytes) and read as 64-bit LDS loads
+enum { CR_J = 0, CR_DIST = CR_J + 3 * CJ, CR_MU, CR_D, CR_KD, CR_BD, CR_POS, CR_FR = CR_POS + 3, CR_VEL = CR_FR + 9,
        CR_JA = CR_VEL + 3, CR_JD = CR_JA + 3, CR_F = CR_JD + 3, CR_N = CR_F + 4,
        CR_K = CR_JD /* 6 slots over JD+F: K_c during the Hessian build only */ };
 // generic row record (equality / joint limit)

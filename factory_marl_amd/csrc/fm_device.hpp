@@ -2259,7 +2259,14 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     PMARK(PH_NGRAD);
     if (scale * sqrt(gn) < tol) break;
     // Hessian H = M + sum_c B_c' K_c B_c + generic rows
-    for (int e = LANE; e < nv * nv; e += WAVE) H[e] = T(0);
+    {
+      // zero fill in 16-byte stores (the region is 16-byte aligned), then the tail
+      constexpr int PER16 = 16 / sizeof(T);
+      const int n16 = nv * nv / PER16;
+      uint4* H16 = (uint4*)H;
+      for (int e = LANE; e < n16; e += WAVE) H16[e] = make_uint4(0u, 0u, 0u, 0u);
+      for (int e = n16 * PER16 + LANE; e < nv * nv; e += WAVE) H[e] = T(0);
+    }
     SYNC();
     {
       int a0 = 1 + 6 * dm.K;
@@ -2275,7 +2282,10 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SYNC();
     // contact blocks B_c' K_c B_c: K_c (3x3, from the active pyramid edges) for every contact at once, then
     // one lane per (contact, block column ii) in fixed slots of CJ, adding its whole block column with LDS
-    // atomics (one wave: deterministic order)
+    // atomics (one wave: deterministic order).  The column's operands are read unconditionally (all inside the
+    // record), so the loads issue as one batch; only the atomics are predicated on the contact's column count.
+    // (Summing consecutive contacts between the same two trees on one lane before the atomics was slower: the
+    // serial per-lane chain costs more than the atomics it saves.)
     contact_K(w, ncon);
     SYNC();
     for (int e = LANE; e < CJ * ncon; e += WAVE) {
@@ -2294,12 +2304,18 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
       const int gi = ii < nda ? oa + ii : ob + ii - nda;
       T* Hrow = H + gi * nv;
+      T jr0[CJ], jr1[CJ], jr2[CJ];
 #pragma unroll
       for (int jj = 0; jj < CJ; jj++) {
-        if (jj < ncol) {
-          const int gj = jj < nda ? oa + jj : ob + jj - nda;
-          atomicAdd(Hrow + gj, q0 * J[jj] + q1 * J[CJ + jj] + q2 * J[2 * CJ + jj]);
-        }
+        jr0[jj] = J[jj];
+        jr1[jj] = J[CJ + jj];
+        jr2[jj] = J[2 * CJ + jj];
+      }
+#pragma unroll
+      for (int jj = 0; jj < CJ; jj++) {
+        const int gj = jj < nda ? oa + jj : ob + jj - nda;
+        const T val = q0 * jr0[jj] + q1 * jr1[jj] + q2 * jr2[jj];
+        if (jj < ncol) atomicAdd(Hrow + gj, val);
       }
     }
     SYNC();
