@@ -1225,10 +1225,6 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
   const T* base = M.arm_base + 12 * arm;
   T* bpos = w.bpos() + 30 * arm;
   T* bR = w.bR() + 90 * arm;
-  T* bcom = w.bcom() + 30 * arm;
-  T* bIw = w.bIw() + 60 * arm;
-  T* bF = w.bF() + 30 * arm;
-  T* bN = w.bN() + 30 * arm;
   T* dax = w.dax() + 27 * arm;
   T* danc = w.danc() + 27 * arm;
   const T p0[3] = {base[0], base[1], base[2]};
@@ -1237,7 +1233,6 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
   for (int k = 0; k < 9; k++) PR[k] = base[3 + k];
   T Pw[3] = {0, 0, 0}, Pal[3] = {0, 0, 0}, Pvo[3] = {0, 0, 0}, Pao[3] = {0, 0, 0};
   T Gp[3], GR[9], Gw[3], Gal[3], Gvo[3], Gao[3];
-  T ax7[3], ax8[3];
 #pragma unroll
   for (int b = 0; b < 10; b++) {
     const double* bl = ARM_BODY[b];
@@ -1312,10 +1307,6 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
         o[k] += ax[k] * q[d];
         dax[3 * d + k] = ax[k];
         danc[3 * d + k] = o[k];
-        if (d == 7)
-          ax7[k] = ax[k];
-        else
-          ax8[k] = ax[k];
       }
 #pragma unroll
       for (int k = 0; k < 9; k++) R[k] = Rpre[k];
@@ -1339,47 +1330,15 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
     for (int k = 0; k < 3; k++) bpos[3 * b + k] = o[k];
 #pragma unroll
     for (int k = 0; k < 9; k++) bR[9 * b + k] = R[k];
-    // com and world inertia
-    T ci[3];
-    matvec3_c(R, bl + 13, ci);
-    T com[3] = {o[0] + ci[0], o[1] + ci[1], o[2] + ci[2]};
-#pragma unroll
-    for (int k = 0; k < 3; k++) bcom[3 * b + k] = com[k];
-    T Ri[9];
-    matmul3_c(R, bl + 16, Ri);
-    const double* I = bl + 25;
-    T Iw[6];
-    Iw[0] = cmul(Ri[0] * Ri[0], I[0]) + cmul(Ri[1] * Ri[1], I[1]) + cmul(Ri[2] * Ri[2], I[2]);
-    Iw[1] = cmul(Ri[3] * Ri[3], I[0]) + cmul(Ri[4] * Ri[4], I[1]) + cmul(Ri[5] * Ri[5], I[2]);
-    Iw[2] = cmul(Ri[6] * Ri[6], I[0]) + cmul(Ri[7] * Ri[7], I[1]) + cmul(Ri[8] * Ri[8], I[2]);
-    Iw[3] = cmul(Ri[0] * Ri[3], I[0]) + cmul(Ri[1] * Ri[4], I[1]) + cmul(Ri[2] * Ri[5], I[2]);
-    Iw[4] = cmul(Ri[0] * Ri[6], I[0]) + cmul(Ri[1] * Ri[7], I[1]) + cmul(Ri[2] * Ri[8], I[2]);
-    Iw[5] = cmul(Ri[3] * Ri[6], I[0]) + cmul(Ri[4] * Ri[7], I[1]) + cmul(Ri[5] * Ri[8], I[2]);
-#pragma unroll
-    for (int k = 0; k < 6; k++) bIw[6 * b + k] = Iw[k];
     if (DYN) {
-      const double mass = bl[12];
-      const T rc[3] = {com[0] - o[0], com[1] - o[1], com[2] - o[2]};
-      T u1[3], u2[3], u3[3];
-      cross3(al, rc, u1);
-      cross3(wv, rc, u2);
-      cross3(wv, u2, u3);
-      T F[3];
-#pragma unroll
-      for (int k = 0; k < 3; k++) F[k] = cmul(ao[k] + u1[k] + u3[k], mass);
-      F[2] += T(mass) * M.grav;
-      T Iwv[3] = {Iw[0] * wv[0] + Iw[3] * wv[1] + Iw[4] * wv[2], Iw[3] * wv[0] + Iw[1] * wv[1] + Iw[5] * wv[2],
-                  Iw[4] * wv[0] + Iw[5] * wv[1] + Iw[2] * wv[2]};
-      T Ial[3] = {Iw[0] * al[0] + Iw[3] * al[1] + Iw[4] * al[2], Iw[3] * al[0] + Iw[1] * al[1] + Iw[5] * al[2],
-                  Iw[4] * al[0] + Iw[5] * al[1] + Iw[2] * al[2]};
-      T gy[3];
-      cross3(wv, Iwv, gy);
-      T cr[3] = {com[0] - p0[0], com[1] - p0[1], com[2] - p0[2]}, mo[3];
-      cross3(cr, F, mo);
+      // the body's angular velocity / acceleration and origin acceleration for the per-body pass
+      // (arm_body_post); the Hessian region is free during kinematics
+      T* sc = w.H() + 90 * arm + 9 * b;
 #pragma unroll
       for (int k = 0; k < 3; k++) {
-        bF[3 * b + k] = F[k];
-        bN[3 * b + k] = mo[k] + Ial[k] + gy[k];
+        sc[k] = wv[k];
+        sc[3 + k] = al[k];
+        sc[6 + k] = ao[k];
       }
     }
     // advance the chain
@@ -1414,27 +1373,97 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
       for (int k = 0; k < 3; k++) w.site()[3 * arm + k] = o[k] + sp[k];
     }
   }
+}
+
+// Per-body part of the arm kinematics, one lane per (arm, body) after arm_chain: com, world inertia and, with
+// DYN, the RNE body force / moment about the arm base (MuJoCo mj_rne, flg_acc = 0).  The same expressions the
+// chain lane evaluated before (body constants now from the scene table, the chain's outputs from LDS).
+template <typename T, typename DIM, bool DYN>
+__device__ __forceinline__ void arm_body_post(const Model<T>& M, const Ws<T, DIM>& w, int arm, int b) {
+  const T* bl = M.body + 32 * b;
+  const T* base = M.arm_base + 12 * arm;
+  const T* o = w.bpos() + 30 * arm + 3 * b;
+  const T* R = w.bR() + 90 * arm + 9 * b;
+  T Rr[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) Rr[k] = R[k];
+  T ci[3];
+  matvec3(Rr, bl + 13, ci);
+  const T com[3] = {o[0] + ci[0], o[1] + ci[1], o[2] + ci[2]};
+  T* bcom = w.bcom() + 30 * arm + 3 * b;
+#pragma unroll
+  for (int k = 0; k < 3; k++) bcom[k] = com[k];
+  T Ri[9];
+  matmul3(Rr, bl + 16, Ri);
+  const T* I = bl + 25;
+  T Iw[6];
+  Iw[0] = Ri[0] * Ri[0] * I[0] + Ri[1] * Ri[1] * I[1] + Ri[2] * Ri[2] * I[2];
+  Iw[1] = Ri[3] * Ri[3] * I[0] + Ri[4] * Ri[4] * I[1] + Ri[5] * Ri[5] * I[2];
+  Iw[2] = Ri[6] * Ri[6] * I[0] + Ri[7] * Ri[7] * I[1] + Ri[8] * Ri[8] * I[2];
+  Iw[3] = Ri[0] * Ri[3] * I[0] + Ri[1] * Ri[4] * I[1] + Ri[2] * Ri[5] * I[2];
+  Iw[4] = Ri[0] * Ri[6] * I[0] + Ri[1] * Ri[7] * I[1] + Ri[2] * Ri[8] * I[2];
+  Iw[5] = Ri[3] * Ri[6] * I[0] + Ri[4] * Ri[7] * I[1] + Ri[5] * Ri[8] * I[2];
+  T* bIw = w.bIw() + 60 * arm + 6 * b;
+#pragma unroll
+  for (int k = 0; k < 6; k++) bIw[k] = Iw[k];
   if (DYN) {
-    SYNC();
-    // backward pass: generalized bias forces of the arm's 9 dofs (RNE, qacc = 0); the per-body records
-    // come back from LDS in one batch of independent reads
-    T* pb = w.pb() + 1 + 6 * dm.K + 9 * arm;
-    pb[7] = -(ax7[0] * bF[24] + ax7[1] * bF[25] + ax7[2] * bF[26]);
-    pb[8] = -(ax8[0] * bF[27] + ax8[1] * bF[28] + ax8[2] * bF[29]);
-    T ft[3] = {0, 0, 0}, nt[3] = {0, 0, 0};
+    const T* sc = w.H() + 90 * arm + 9 * b;
+    const T wv[3] = {sc[0], sc[1], sc[2]}, al[3] = {sc[3], sc[4], sc[5]}, ao[3] = {sc[6], sc[7], sc[8]};
+    const T mass = bl[12];
+    const T rc[3] = {com[0] - o[0], com[1] - o[1], com[2] - o[2]};
+    T u1[3], u2[3], u3[3];
+    cross3(al, rc, u1);
+    cross3(wv, rc, u2);
+    cross3(wv, u2, u3);
+    T F[3];
 #pragma unroll
-    for (int b = 9; b >= 0; b--) {
+    for (int k = 0; k < 3; k++) F[k] = (ao[k] + u1[k] + u3[k]) * mass;
+    F[2] += mass * M.grav;
+    T Iwv[3] = {Iw[0] * wv[0] + Iw[3] * wv[1] + Iw[4] * wv[2], Iw[3] * wv[0] + Iw[1] * wv[1] + Iw[5] * wv[2],
+                Iw[4] * wv[0] + Iw[5] * wv[1] + Iw[2] * wv[2]};
+    T Ial[3] = {Iw[0] * al[0] + Iw[3] * al[1] + Iw[4] * al[2], Iw[3] * al[0] + Iw[1] * al[1] + Iw[5] * al[2],
+                Iw[4] * al[0] + Iw[5] * al[1] + Iw[2] * al[2]};
+    T gy[3];
+    cross3(wv, Iwv, gy);
+    T cr[3] = {com[0] - base[0], com[1] - base[1], com[2] - base[2]}, mo[3];
+    cross3(cr, F, mo);
+    T* bF = w.bF() + 30 * arm + 3 * b;
+    T* bN = w.bN() + 30 * arm + 3 * b;
 #pragma unroll
-      for (int k = 0; k < 3; k++) {
-        ft[k] += bF[3 * b + k];
-        nt[k] += bN[3 * b + k];
-      }
-      if (b <= 6) {
-        T ar[3] = {danc[3 * b] - p0[0], danc[3 * b + 1] - p0[1], danc[3 * b + 2] - p0[2]}, af[3];
-        cross3(ar, ft, af);
-        T tn[3] = {nt[0] - af[0], nt[1] - af[1], nt[2] - af[2]};
-        pb[b] = -dot3(dax + 3 * b, tn);
-      }
+    for (int k = 0; k < 3; k++) {
+      bF[k] = F[k];
+      bN[k] = mo[k] + Ial[k] + gy[k];
+    }
+  }
+}
+
+// RNE backward pass of one arm (one lane per arm, after arm_body_post): generalized bias forces of the arm's
+// 9 dofs (qacc = 0); the per-body records come back from LDS in one batch of independent reads
+template <typename T, typename DIM>
+__device__ __forceinline__ void arm_rne_back(const Model<T>& M, const Ws<T, DIM>& w, int arm) {
+  const DIM dm(M.dm);
+  const T* base = M.arm_base + 12 * arm;
+  const T p0[3] = {base[0], base[1], base[2]};
+  const T* bF = w.bF() + 30 * arm;
+  const T* bN = w.bN() + 30 * arm;
+  const T* dax = w.dax() + 27 * arm;
+  const T* danc = w.danc() + 27 * arm;
+  T* pb = w.pb() + 1 + 6 * dm.K + 9 * arm;
+  pb[7] = -(dax[21] * bF[24] + dax[22] * bF[25] + dax[23] * bF[26]);
+  pb[8] = -(dax[24] * bF[27] + dax[25] * bF[28] + dax[26] * bF[29]);
+  T ft[3] = {0, 0, 0}, nt[3] = {0, 0, 0};
+#pragma unroll
+  for (int b = 9; b >= 0; b--) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      ft[k] += bF[3 * b + k];
+      nt[k] += bN[3 * b + k];
+    }
+    if (b <= 6) {
+      T ar[3] = {danc[3 * b] - p0[0], danc[3 * b + 1] - p0[1], danc[3 * b + 2] - p0[2]}, af[3];
+      cross3(ar, ft, af);
+      T tn[3] = {nt[0] - af[0], nt[1] - af[1], nt[2] - af[2]};
+      pb[b] = -dot3(dax + 3 * b, tn);
     }
   }
 }
@@ -1523,6 +1552,11 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     pb[3] = pb[4] = pb[5] = 0;
   }
   if (LANE == 0) w.pb()[0] = -M.belt_damp * v[0];  // belt: damping, no gravity along y
+  SYNC();
+  // per-body com / inertia / RNE forces one lane per (arm, body), then the RNE backward sum one lane per arm
+  for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, true>(M, w, e / 10, e % 10);
+  SYNC();
+  if (LANE < A) arm_rne_back(M, w, LANE);
   SYNC();
   PMARK(PH_FK);
   // ---- actuator length / velocity (transmission at the stage state)
@@ -3110,6 +3144,8 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     }
     // gripper sites at the final state (the last mj_step1's site_xpos)
     if (LANE < A) arm_chain<T, DIM, false>(M, w, LANE);
+    SYNC();
+    for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, false>(M, w, e / 10, e % 10);
     SYNC();
     // stage state for the next env-step = state before the TaskManager's teleports
     for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
