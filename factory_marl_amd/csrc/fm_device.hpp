@@ -1207,6 +1207,22 @@ __device__ __forceinline__ void matmul3_c(const T* A, const double* B, T* C) {
       C[3 * i + j] = cmul(A[3 * i], B[j]) + cmul(A[3 * i + 1], B[3 + j]) + cmul(A[3 * i + 2], B[6 + j]);
 }
 
+// sin / cos of the 7 hinge angles of every arm, one lane per hinge, ahead of the serial chain (the Hessian
+// region is free during kinematics and holds nv^2 >= 104 A reals: arm_body_post's 90 per arm, then these 14)
+template <typename T, typename DIM>
+__device__ __forceinline__ T* arm_hinge_sc(const Ws<T, DIM>& w, int A, int arm) {
+  return w.H() + 90 * A + 14 * arm;
+}
+template <typename T, typename DIM>
+__device__ __forceinline__ void arm_hinge_sincos(const Model<T>& M, const Ws<T, DIM>& w) {
+  const DIM dm(M.dm);
+  for (int e = LANE; e < 7 * dm.A; e += WAVE) {
+    const int arm = e / 7, j = e - 7 * arm;
+    T* sc = arm_hinge_sc(w, dm.A, arm) + 2 * j;
+    sincos_t(w.q()[1 + 7 * dm.K + 9 * arm + j], sc, sc + 1);
+  }
+}
+
 // Forward kinematics (+ RNE when DYN) of one arm on one lane: link1..7 (hinges about local z), the gripper
 // base (welded), the two plates (slides along local x) -- iiwa14.xml:62-139, gripper.xml:9-42.  Body poses,
 // joint axes/anchors, coms, world inertias, gripper site to LDS; DYN adds the RNE bias forces (qacc = 0)
@@ -1216,6 +1232,7 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
   const DIM dm(M.dm);
   const T* qa = w.q() + 1 + 7 * dm.K + 9 * arm;
   const T* va = w.v() + 1 + 6 * dm.K + 9 * arm;
+  const T* hsc = arm_hinge_sc(w, dm.A, arm);
   T q[9], qd[9];
 #pragma unroll
   for (int k = 0; k < 9; k++) {
@@ -1270,8 +1287,7 @@ __device__ __forceinline__ void arm_chain(const Model<T>& M, const Ws<T, DIM>& w
         dax[3 * b + k] = ax[k];
         danc[3 * b + k] = o[k];
       }
-      T sn, cs;
-      sincos_t(q[b], &sn, &cs);
+      const T sn = hsc[2 * b], cs = hsc[2 * b + 1];
 #pragma unroll
       for (int rr = 0; rr < 3; rr++) {
         R[3 * rr + 0] = Rpre[3 * rr + 0] * cs + Rpre[3 * rr + 1] * sn;
@@ -1521,6 +1537,8 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   T* q = w.q();
   T* v = w.v();
   // ---- kinematics + RNE (one lane per arm), cubes (one lane per cube)
+  arm_hinge_sincos(M, w);
+  SYNC();
   if (LANE < A) arm_chain<T, DIM, true>(M, w, LANE);
   for (int k = LANE; k < K; k += WAVE) {
     T* qq = q + 1 + 7 * k;
@@ -3143,6 +3161,8 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
       if (LANE == 0) sc_[3] = __ballot(hit) != 0ull ? 1.0 : 0.0;
     }
     // gripper sites at the final state (the last mj_step1's site_xpos)
+    arm_hinge_sincos(M, w);
+    SYNC();
     if (LANE < A) arm_chain<T, DIM, false>(M, w, LANE);
     SYNC();
     for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, false>(M, w, e / 10, e % 10);
