@@ -1597,9 +1597,42 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     w.alen()[u] = L;
     w.avel()[u] = V;
   }
-  // ---- arm mass-matrix blocks: M_ij = sum_{b in desc} m Jc_i.Jc_j + Jr_i' Iw Jr_j, one entry (i >= j) per
-  // lane; the body loop is unrolled (masses are immediates, every LDS read independent), bodies outside the
-  // subtree of dof i are selected away
+  // ---- arm mass-matrix blocks, composite-rigid-body style.  Hinge i moves the bodies b >= i; about its anchor
+  // p_i their composite mass moment h_i = sum m r and inertia J_i = sum Iw + m (|r|^2 1 - r r'), r = com - p_i
+  // (one lane per hinge; the Hessian region is free before the collision).  Then one entry (i >= j) per lane:
+  //   hinges i >= j:  M_ij = a_i' J_i a_j + (a_i x h_i) . (a_j x (p_i - p_j))
+  //   slide i (its plate only):  M_ij = m (a_i . c_j), c_j = a_j x (com - p_j) for a hinge j, a_i for j = i.
+  // Same sums as sum_{b in desc} m Jc_i.Jc_j + Jr_i' Iw Jr_j, regrouped per subtree.
+  for (int e = LANE; e < 7 * A; e += WAVE) {
+    const int arm = e / 7, i = e - 7 * arm;
+    const T* danc = w.danc() + 27 * arm;
+    const T* bcom = w.bcom() + 30 * arm;
+    const T* bIw = w.bIw() + 60 * arm;
+    const T pi[3] = {danc[3 * i], danc[3 * i + 1], danc[3 * i + 2]};
+    T mh[3] = {0, 0, 0}, J[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 10; b++) {
+      const T* com = bcom + 3 * b;
+      const T* Iw = bIw + 6 * b;
+      const T m = T(ARM_BODY[b][12]);
+      const T r[3] = {com[0] - pi[0], com[1] - pi[1], com[2] - pi[2]};
+      const T mr[3] = {m * r[0], m * r[1], m * r[2]};
+      const T rr = r[0] * mr[0] + r[1] * mr[1] + r[2] * mr[2];
+      const T t[6] = {Iw[0] + rr - r[0] * mr[0], Iw[1] + rr - r[1] * mr[1], Iw[2] + rr - r[2] * mr[2],
+                      Iw[3] - r[0] * mr[1], Iw[4] - r[0] * mr[2], Iw[5] - r[1] * mr[2]};
+      const bool in = b >= i;
+#pragma unroll
+      for (int k = 0; k < 3; k++) mh[k] += in ? mr[k] : T(0);
+#pragma unroll
+      for (int k = 0; k < 6; k++) J[k] += in ? t[k] : T(0);
+    }
+    T* sc = w.H() + 9 * (7 * arm + i);
+#pragma unroll
+    for (int k = 0; k < 3; k++) sc[k] = mh[k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) sc[3 + k] = J[k];
+  }
+  SYNC();
   for (int e = LANE; e < 45 * A; e += WAVE) {
     const int arm = e / 45;
     const int t = e - 45 * arm;
@@ -1609,38 +1642,33 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     const int j = t - i * (i + 1) / 2;
     const T* dax = w.dax() + 27 * arm;
     const T* danc = w.danc() + 27 * arm;
-    const T* bcom = w.bcom() + 30 * arm;
-    const T* bIw = w.bIw() + 60 * arm;
     const T ai[3] = {dax[3 * i], dax[3 * i + 1], dax[3 * i + 2]}, aj[3] = {dax[3 * j], dax[3 * j + 1], dax[3 * j + 2]};
-    const T pi[3] = {danc[3 * i], danc[3 * i + 1], danc[3 * i + 2]};
     const T pj[3] = {danc[3 * j], danc[3 * j + 1], danc[3 * j + 2]};
-    const bool hi_i = i <= 6, hi_j = j <= 6;
-    T s = 0;
-#pragma unroll
-    for (int b = 0; b < 10; b++) {
-      const bool in = (hi_i ? b >= i : b == i + 1) && (hi_j ? b >= j : b == j + 1);
-      const T* com = bcom + 3 * b;
-      const T* Iw = bIw + 6 * b;
-      const T ri[3] = {com[0] - pi[0], com[1] - pi[1], com[2] - pi[2]};
-      const T rj[3] = {com[0] - pj[0], com[1] - pj[1], com[2] - pj[2]};
-      T ci[3], cj[3];
-      cross3(ai, ri, ci);
-      cross3(aj, rj, cj);
-      if (!hi_i) {
-        ci[0] = ai[0];
-        ci[1] = ai[1];
-        ci[2] = ai[2];
+    T s;
+    if (i <= 6) {
+      const T* sc = w.H() + 9 * (7 * arm + i);
+      const T pi[3] = {danc[3 * i], danc[3 * i + 1], danc[3 * i + 2]};
+      const T Ja[3] = {sc[3] * aj[0] + sc[6] * aj[1] + sc[7] * aj[2], sc[6] * aj[0] + sc[4] * aj[1] + sc[8] * aj[2],
+                       sc[7] * aj[0] + sc[8] * aj[1] + sc[5] * aj[2]};
+      const T h[3] = {sc[0], sc[1], sc[2]}, d[3] = {pi[0] - pj[0], pi[1] - pj[1], pi[2] - pj[2]};
+      T ah[3], ad[3];
+      cross3(ai, h, ah);
+      cross3(aj, d, ad);
+      s = dot3(ai, Ja) + dot3(ah, ad);
+    } else {
+      const int b = i + 1;  // the plate
+      const T* com = w.bcom() + 30 * arm + 3 * b;
+      T cj[3];
+      if (j <= 6) {
+        const T rj[3] = {com[0] - pj[0], com[1] - pj[1], com[2] - pj[2]};
+        cross3(aj, rj, cj);
+      } else {
+        cj[0] = j == i ? aj[0] : T(0);
+        cj[1] = j == i ? aj[1] : T(0);
+        cj[2] = j == i ? aj[2] : T(0);
       }
-      if (!hi_j) {
-        cj[0] = aj[0];
-        cj[1] = aj[1];
-        cj[2] = aj[2];
-      }
-      T term = T(ARM_BODY[b][12]) * dot3(ci, cj);
-      const T Ir[3] = {Iw[0] * aj[0] + Iw[3] * aj[1] + Iw[4] * aj[2], Iw[3] * aj[0] + Iw[1] * aj[1] + Iw[5] * aj[2],
-                       Iw[4] * aj[0] + Iw[5] * aj[1] + Iw[2] * aj[2]};
-      if (hi_i && hi_j) term += dot3(ai, Ir);
-      s += in ? term : T(0);
+      static_assert(ARM_BODY[8][12] == ARM_BODY[9][12], "the two plates are assumed to weigh the same");
+      s = T(ARM_BODY[8][12]) * dot3(ai, cj);
     }
     T* Ma = w.Marm() + 81 * arm;
     Ma[9 * i + j] = s;
