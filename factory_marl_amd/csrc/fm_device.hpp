@@ -1029,29 +1029,23 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   uint32_t* sp = w.sp();
   int nsp = 0, total = 0;
   auto sweep = [&](uint32_t bpw, int pidx) {
-    bool hit = false;
-    int ncomb = 0;
-    if (pidx < dm.ncbp) {
-      const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
-      const T* X = w.cbw() + 8 * b1;
-      const T* Y = w.cbw() + 8 * b2;
-      const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1];
-      if (f1 & CB_PLANE) {
-        hit = Y[2] - Y[6] - Y[3] <= T(0);
-      } else if (f2 & CB_PLANE) {
-        hit = X[2] - X[6] - X[3] <= T(0);
-      } else {
-        T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
-        T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
-        T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
-        d0 = d0 > T(0) ? d0 : T(0);
-        d1 = d1 > T(0) ? d1 : T(0);
-        d2 = d2 > T(0) ? d2 : T(0);
-        T rr = X[3] + Y[3];
-        hit = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
-      }
-      if (hit) ncomb = cbi[4 * b1 + 3] * cbi[4 * b2 + 3];
-    }
+    // branch-free: both records and both flag words are read unconditionally (a lane past the list reads body
+    // 0's), so each pass is one batch of LDS reads
+    const int b1 = bpw & 255, b2 = (bpw >> 8) & 255;
+    const T* X = w.cbw() + 8 * b1;
+    const T* Y = w.cbw() + 8 * b2;
+    const int f1 = cbi[4 * b1 + 1], f2 = cbi[4 * b2 + 1], n1 = cbi[4 * b1 + 3], n2 = cbi[4 * b2 + 3];
+    T d0 = fabs(X[0] - Y[0]) - X[4] - Y[4];
+    T d1 = fabs(X[1] - Y[1]) - X[5] - Y[5];
+    T d2 = fabs(X[2] - Y[2]) - X[6] - Y[6];
+    d0 = d0 > T(0) ? d0 : T(0);
+    d1 = d1 > T(0) ? d1 : T(0);
+    d2 = d2 > T(0) ? d2 : T(0);
+    const T rr = X[3] + Y[3];
+    const bool hs = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
+    const bool hp1 = Y[2] - Y[6] - Y[3] <= T(0), hp2 = X[2] - X[6] - X[3] <= T(0);
+    const bool hit = pidx < dm.ncbp && ((f1 & CB_PLANE) ? hp1 : ((f2 & CB_PLANE) ? hp2 : hs));
+    const int ncomb = hit ? n1 * n2 : 0;
     const uint64_t bal = __ballot(hit);
     const int incl = wave_incl_scan(ncomb);
     if (hit) sp[nsp + __popcll(bal & below)] = (bpw & 0xFFFFu) | ((uint32_t)(total + incl - ncomb) << 16);
