@@ -5,25 +5,39 @@ Metric (BASELINE.json): env-steps/sec (whole node), 4096 arenas 2-arm x 4-obj, 1
 Workload (BASELINE.md / SURVEY.md §8d, config 2): 4096 arenas per GPU, A=2 arms, K=4 cubes,
 AllFullRLProgressRewardEnv, random policy U[-1,1]^16 drawn from a Philox stream (seed 0 + rank) before the
 timed region (policy excluded), auto-reset inside the step.  One step = one env-step of every arena
-(100 physics substeps + task layer).  Multi-GPU: one process per GPU, arenas are independent (weak
-scaling, no data-path collective); value = all ranks' env-steps / max-over-ranks time.
+(100 physics substeps + task layer).  Multi-GPU: one process per GPU (factory_marl_amd/launch.py), arenas
+are independent (weak scaling, no data-path collective); value = all ranks' env-steps / max-over-ranks time.
+
+Episode mix: all arenas start from reset in lockstep, so before timing every arena is pre-rolled with
+random actions and reset once at a random offset (masked fm_reset) -- the timed window then holds arenas
+at every episode phase (cube counts, contacts, terminations and auto-resets in their stationary mix,
+reported under "diagnostics") instead of the first seconds of one synchronised episode.
 
 Roofline: the dominant (only) kernel in the timed region is fm::step_kernel; its average launch time is
 measured with HIP events on the stream it runs on.  Algorithmic bytes per arena env-step
-B(A,K) = 100*8*(nq + 2nv + nu) + 4*(act_dim + obs_dim + 4) = 120,480 B at (2,4).
+B(A,K) = 100*8*(nq + 2nv + nu) + 4*(act_dim + obs_dim + 4) = 120,480 B at (2,4).  The
+kernel is bound by neither HBM nor MFMA but by dependent LDS / VALU latency chains at one wave per SIMD;
+"roofline.valu" prices its VALU work (PMC instruction counts per arena env-step, profiles/) against the
+fp32 vector peak with the live kernel time.
 CPU baseline: the oracle (our C restatement of the reference algorithm, oracle/) stepped with OpenMP on
 the host cores of the same box, on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+from factory_marl_amd.launch import (RankContext, arena_seeds, job_throughput, max_over_ranks,  # noqa: E402,F401
+                                     rank_arenas)
+
+HBM_PEAK_GBPS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector peak (same table)
+FP64_PEAK_TFLOPS = 78.6    # fp64 vector rate = 1/2 of fp32
 
 
 def algorithmic_bytes(A, K):
@@ -32,21 +46,15 @@ def algorithmic_bytes(A, K):
     return 100 * 8 * (nq + 2 * nv + nu) + 4 * (act_dim + obs_dim + 4)
 
 
-def max_over_ranks(x, device=None):
-    """max of a host float over all ranks (the slowest rank's clock sets the job time); identity at N=1"""
-    import torch
-    import torch.distributed as dist
-
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device if device is not None else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def job_throughput(arenas_per_rank, steps, world, wall_max):
-    """whole-job env-steps/s: every rank steps its own arenas (weak scaling, no data-path collective)"""
-    return world * arenas_per_rank * steps / wall_max
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return "unknown"
 
 
 def cpu_baseline(A, K, seconds):
@@ -65,8 +73,84 @@ def cpu_baseline(A, K, seconds):
     steps = max(2, int(rate * seconds / cores))
     dt = L.or_batch_bench(A, K, cores, steps, cores, 0, C.byref(n))
     return {"value": round(n.value / dt, 3), "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{cores} arenas x {steps} env-steps ({A} arms x {K} objects, random actions), "
-                      f"oracle/ C restatement (fp64, OpenMP), {dt:.1f} s wall"}
+                      f"oracle/ C restatement (fp64, dense Cholesky, OpenMP), {dt:.1f} s wall"}
+
+
+def preroll(env, steps, rank, device):
+    """desynchronise the arenas: random actions, each arena reset once at a random offset in [0, steps)"""
+    import numpy as np
+    import torch
+
+    if steps <= 0:
+        return
+    N = env.num_envs
+    off = np.random.default_rng(1234 + rank).integers(0, steps, N)
+    g = torch.Generator(device=device)
+    g.manual_seed(10_000 + rank)
+    for s in range(steps):
+        m = (off == s).astype(np.uint8)
+        if m.any():
+            env.reset(mask=m)
+        env.step_tensors(torch.rand(N, env.act_dim, device=device, generator=g) * 2.0 - 1.0)
+
+
+def timed_run(ctx, args, precision, steps, warmup, lo, hi):
+    """build, pre-roll, warm up and time `steps` env-steps of this rank's arenas; returns (wall, kernel ms,
+    counter deltas over the timed window)"""
+    import torch
+
+    from factory_marl_amd import FactoryVecEnv
+
+    A, K, N = args.arms, args.objects, hi - lo
+    env = FactoryVecEnv(N, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42), device=ctx.local_rank,
+                        precision=precision, seeds=arena_seeds(lo, hi, args.seeds))
+    env.reset()
+    preroll(env, args.preroll, ctx.rank, ctx.device)
+    g = torch.Generator(device=ctx.device)
+    g.manual_seed(0 + ctx.rank)
+    total = warmup + steps
+    acts = torch.rand(total, N, env.act_dim, device=ctx.device, generator=g, dtype=torch.float32) * 2.0 - 1.0
+    for s in range(warmup):
+        env.step_tensors(acts[s])
+    torch.cuda.synchronize()
+    c0 = env.counters()
+    ctx.barrier()
+    stream = torch.cuda.current_stream(ctx.device)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in range(warmup, total):
+        env.step_tensors(acts[s])
+    ev1.record(stream)
+    ctx.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / steps  # average step_kernel launch (the only kernel in the region)
+    dc = env.counters() - c0
+    env.close()
+    return wall, kern_ms, dc
+
+
+def diagnostics(dc, N, steps, frame_skip=100):
+    es = N * steps
+    return {"env_steps_timed": es,
+            "mean_objects_in_scene": round(float(dc[:, 6].sum()) / es, 3),
+            "episodes_ended": int(dc[:, 7].sum()),
+            "mean_contacts_per_substep": round(float(dc[:, 4].sum()) / (es * frame_skip), 3),
+            "max_contacts_in_a_substep": int(dc[:, 5].max()) if len(dc) else 0,
+            "contacts_dropped": int(dc[:, 0].sum()),
+            "newton_iters_per_substep": round(float(dc[:, 1].sum()) / (es * frame_skip), 3),
+            "newton_maxiter_hits": int(dc[:, 2].sum())}
+
+
+def load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -78,80 +162,61 @@ def main():
     ap.add_argument("--arms", type=int, default=2)
     ap.add_argument("--objects", type=int, default=4)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--preroll", type=int, default=200, help="env-steps of desynchronising pre-roll")
+    ap.add_argument("--seeds", default="fixed", choices=["fixed", "arena"],
+                    help="scene/TaskManager seed: 42 everywhere (saved runs) or 42 + global arena id")
+    ap.add_argument("--fp64-steps", type=int, default=30, help="also time the fp64 build (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "pmc_valu.json"),
+                    help="VALU instruction counts per arena env-step by rocprofv3 --pmc (tools/pmc_valu.py)")
     args = ap.parse_args()
 
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
-    torch.cuda.set_device(device)
-
-    from factory_marl_amd import FactoryVecEnv
-
+    ctx = RankContext.from_env()
     A, K, N = args.arms, args.objects, args.arenas
-    env = FactoryVecEnv(N, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42), device=local_rank,
-                        precision=args.precision)
-    env.reset()
-    g = torch.Generator(device=device)
-    g.manual_seed(0 + rank)
-    total = args.warmup + args.steps
-    acts = torch.rand(total, N, env.act_dim, device=device, generator=g, dtype=torch.float32) * 2.0 - 1.0
-    for s in range(args.warmup):
-        env.step_tensors(acts[s])
-    torch.cuda.synchronize()
-
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    stream = torch.cuda.current_stream(device)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for s in range(args.warmup, total):
-        env.step_tensors(acts[s])
-    ev1.record(stream)
-    barrier()
-    t1 = time.perf_counter()
-    wall = t1 - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # average step_kernel launch (only kernel in the region)
-    wall = max_over_ranks(wall, device)
-    value = job_throughput(N, args.steps, world, wall)
-    ctr = env.counters()
-    dropped = int(ctr[:, 0].sum())
-    diag = {"contacts_dropped": dropped, "newton_iters_per_substep": round(float(ctr[:, 1].sum()) / (N * total * 100), 3),
-            "newton_maxiter_hits": int(ctr[:, 2].sum()), "arenas_with_maxiter": int((ctr[:, 2] > 0).sum())}
-    if rank == 0:
+    lo, hi = rank_arenas(N, ctx.world, ctx.rank, "weak")
+    wall, kern_ms, dc = timed_run(ctx, args, args.precision, args.steps, args.warmup, lo, hi)
+    wall = ctx.max_over_ranks(wall)
+    value = job_throughput(N, args.steps, ctx.world, wall)
+    diag = diagnostics(dc, N, args.steps)
+    fp64 = None
+    if args.fp64_steps > 0 and args.precision == "fp32":
+        w64, k64, dc64 = timed_run(ctx, args, "fp64", args.fp64_steps, min(args.warmup, 5), lo, hi)
+        w64 = ctx.max_over_ranks(w64)
+        fp64 = {"value": round(job_throughput(N, args.fp64_steps, ctx.world, w64), 2), "steps": args.fp64_steps,
+                "ms_per_step": round(w64 / args.fp64_steps * 1e3, 4), "kernel_ms_avg": round(k64, 4),
+                "diagnostics": diagnostics(dc64, N, args.fp64_steps)}
+    if ctx.rank == 0:
         B = algorithmic_bytes(A, K)
         achieved = N * B / (kern_ms * 1e-3) / 1e9
+        tj = load_json(args.traffic_json) or {}
         traffic = None
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("arenas") == N and tj.get("precision") == args.precision and tj.get("A") == A and tj.get("K") == K:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
+        if tj.get("arenas") == N and tj.get("precision") == args.precision and tj.get("A") == A and tj.get("K") == K:
+            traffic = tj.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
+                "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
+                "algorithmic_bytes_per_arena_step": B,
+                "binding": "neither HBM nor MFMA: dependent LDS/VALU latency chains, one wave (arena) per SIMD"}
+        vj = load_json(args.valu_json) or {}
+        if vj.get("A") == A and vj.get("K") == K and vj.get("precision") == args.precision:
+            flops = vj["valu_lane_flops_per_arena_step"] * N
+            vinst = vj["valu_wave_instr_per_arena_step"] * N
+            t = kern_ms * 1e-3
+            peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else FP64_PEAK_TFLOPS
+            roof["valu"] = {"achieved": round(flops / t / 1e12, 4), "peak": peak, "unit": "TFLOP/s",
+                            "frac": round(flops / t / 1e12 / peak, 5),
+                            "issue_frac": round(vinst * 2 / (t * 2.4e9 * 256 * 4), 5),
+                            "note": "lane FLOPs of executed fp32 VALU instructions (all 64 lanes counted) and "
+                                    "VALU issue cycles (2 per wave-instruction) over the chip's SIMD-cycles at "
+                                    "2.4 GHz; counts per arena env-step from " + os.path.relpath(args.valu_json, ROOT)}
         line = {
             "metric": "env-steps/sec (whole node), 4096 arenas 2-arm×4-obj; 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "env-steps/s",
-            "n_gpus": world,
+            "n_gpus": ctx.world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -159,23 +224,21 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "fp32" else "f64",
-            "data": "synthetic (random U[-1,1] AllFullRL actions, Philox seed 0+rank; scene seed 42)",
+            "data": f"synthetic (random U[-1,1] AllFullRL actions, Philox seed 0+rank; scene seed "
+                    f"{'42' if args.seeds == 'fixed' else '42+arena id'}; {args.preroll}-step desynchronising pre-roll)",
             "config": {"workload": f"config 2: {N} arenas/GPU, {A} arms x {K} objects, AllFullRLProgressRewardEnv, "
-                                   "random policy, 100 substeps/env-step, auto-reset",
+                                   "random policy, 100 substeps/env-step, auto-reset, stationary episode mix",
                        "arenas_per_gpu": N, "num_arms": A, "max_num_objects": K,
-                       "parallelism": f"arena-sharded x{world} (no collective)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
-                         "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
-                         "algorithmic_bytes_per_arena_step": B},
+                       "parallelism": f"arena-sharded x{ctx.world} (no collective)"},
+            "roofline": roof,
             "diagnostics": diag,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if fp64 is not None:
+            line["fp64_value"] = fp64
+        if ctx.world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(A, K, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    env.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 
 The reference steps one MuJoCo arena per Python process (challenge_env BaseEnv.step_sim +
 src/environments.py wrappers, driven by SB3 SubprocVecEnv).  Here every arena lives in HBM and one
-hand-written HIP kernel (csrc/fm_kernel.hip) advances all of them per env-step; FactoryVecEnv exposes
+hand-written HIP kernel (csrc/fm_device.hpp, instantiated by csrc/fm_api.hip and csrc/fm_fixed.hip) advances all of them per env-step; FactoryVecEnv exposes
 the SB3 VecEnv surface over it.  See DESIGN.md.
 """
 from ._lib import FactorySimError, load  # noqa: F401

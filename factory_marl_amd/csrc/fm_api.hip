@@ -39,8 +39,9 @@ struct fm_handle {
   SceneHost sc;
   Dims dm;
   int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
+  hipStream_t stream = nullptr;      // stream every call runs on (the private one or the caller's)
+  hipStream_t own_stream = nullptr;  // the private stream fm_create made; the only one fm_destroy destroys
+  hipEvent_t handoff = nullptr;      // orders a new stream after the work queued on the previous one
   bool fp64 = false;
   bool was_reset = false;
   Lay lay;
@@ -146,7 +147,8 @@ static Model<T> make_model(const fm_handle* h) {
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
   const char* cl = getenv("FM_CHOL_LDS");
-  M.dbg_flags = (cl && cl[0] == '1') ? 1 : 0;
+  const char* ng = getenv("FM_NO_NOISE_GUARD");  // experiments: fp32 Newton without the cost-noise stop
+  M.dbg_flags = ((cl && cl[0] == '1') ? 1 : 0) | ((ng && ng[0] == '1') ? 2 : 0);
   return M;
 }
 
@@ -267,9 +269,9 @@ static int create_typed(fm_handle* h) {
   h->allocs.push_back(h->ints);
   HIPCHK(hipMemset(h->ints, 0, N * d.int_stride * sizeof(int32_t)));
   if ((r = upload_raw<uint64_t>(h, &h->rng, s.rng_init))) return r;
-  HIPCHK(hipMalloc((void**)&h->counters, N * 4 * sizeof(int64_t)));
+  HIPCHK(hipMalloc((void**)&h->counters, N * FM_NCTR * sizeof(int64_t)));
   h->allocs.push_back(h->counters);
-  HIPCHK(hipMemset(h->counters, 0, N * 4 * sizeof(int64_t)));
+  HIPCHK(hipMemset(h->counters, 0, N * FM_NCTR * sizeof(int64_t)));
   h->lay = lds_layout(d, sizeof(T));
   if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
   HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -448,11 +450,15 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
     delete h;
     return set_err(FM_EDEVICE, "hipSetDevice failed");
   }
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return set_err(FM_EDEVICE, "hipStreamCreate failed");
   }
-  h->own_stream = true;
+  h->stream = h->own_stream;
+  if (hipEventCreateWithFlags(&h->handoff, hipEventDisableTiming) != hipSuccess) {
+    fm_destroy(h);
+    return set_err(FM_EDEVICE, "hipEventCreate failed");
+  }
   int r = h->fp64 ? create_typed<double>(h) : create_typed<float>(h);
   if (r) {
     std::string e = g_err;
@@ -466,15 +472,25 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
 void fm_destroy(fm_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  // the arena state may still be in use by work queued on the current stream (the caller's or ours)
+  (void)hipStreamSynchronize(h->stream);
+  if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
   for (void* p : h->allocs) (void)hipFree(p);
-  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->handoff) (void)hipEventDestroy(h->handoff);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);  // never a stream the caller handed in
   delete h;
 }
 
 int fm_set_stream(fm_handle* h, void* stream) {
   if (!h) return set_err(FM_EINVAL, "null handle");
-  h->stream = (hipStream_t)stream;  // NULL = the legacy default stream (torch's default stream)
+  hipStream_t next = (hipStream_t)stream;  // NULL = the legacy default stream (torch's default stream)
+  if (next == h->stream) return FM_OK;
+  // arena state is shared by every call of the handle: work queued on the new stream must not start
+  // before what is already queued on the old one (a step on stream B racing a step on stream A)
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipEventRecord(h->handoff, h->stream));
+  HIPCHK(hipStreamWaitEvent(next, h->handoff, 0));
+  h->stream = next;
   return FM_OK;
 }
 
@@ -614,7 +630,7 @@ int fm_get_counters(fm_handle* h, int64_t* host_out) {
   if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * FM_NCTR * sizeof(int64_t), hipMemcpyDeviceToHost));
   return FM_OK;
 }
 

@@ -98,7 +98,8 @@ struct Model {
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
-  int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one
+  int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one, bit 1 = no fp32
+                             // cost-noise stop in Newton (FM_NO_NOISE_GUARD=1)
 };
 
 template <typename T>
@@ -195,7 +196,12 @@ enum { RR_C0 = 0, RR_C1, RR_POS, RR_D, RR_AREF, RR_JAR, RR_JD, RR_F, RR_N };
 // phase slots of the optional wall-clock profile (fm_profile)
 enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_NHESS, PH_NCHOL, PH_NSOLVE, PH_NLS,
        PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_LAST };
-enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE };
+enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE, MISC_CSUM,
+       MISC_CMAX };
+// per-arena int64 counters (fm_get_counters): contacts dropped for capacity, Newton iterations, Newton
+// max-iteration hits, bucket-index anomalies, contacts summed over stages, max contacts in one stage,
+// objects in scene summed over env-steps, episodes ended
+constexpr int FM_NCTR = 8;
 // packed geom info
 enum { GC_PLANE = 0, GC_SPHERE = 1, GC_BOX = 2, GI_ARM = 2, GI_PC = 3 };
 

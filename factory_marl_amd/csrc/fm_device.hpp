@@ -51,11 +51,19 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 #define LANE ((int)threadIdx.x)
-// A workgroup is exactly one wave, and a wave's LDS instructions execute in issue order, so LDS
-// hand-offs between lanes need only a compiler barrier (no s_barrier, no waitcnt-draining fences).
+// A workgroup is exactly one wave.  Lanes hand data to each other through LDS at SYNC(): a
+// wavefront-scope release fence, the wave barrier, a wavefront-scope acquire fence.  The fences order
+// every memory access before the barrier ahead of every access after it (the compiler may not move LDS
+// or global accesses across them, nor forward a stored value past them); at wavefront scope they need no
+// s_waitcnt and no s_barrier, since a wave's LDS instructions execute in issue order.
 // FULL_SYNC() (a real workgroup barrier with memory fences) is kept where lanes hand data to each
 // other through GLOBAL memory: the lane-0 task layer's records read back by the observation writer.
-#define SYNC() asm volatile("" ::: "memory")
+#define SYNC()                                              \
+  do {                                                      \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  \
+    __builtin_amdgcn_wave_barrier();                        \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  \
+  } while (0)
 #define FULL_SYNC() __syncthreads()
 
 template <typename T, typename DIM>
@@ -1171,6 +1179,8 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   if (LANE == 0) {
     misc[MISC_NCON] = ncon;
     misc[MISC_NROW] = 0;
+    misc[MISC_CSUM] += nst;  // contact demand of this stage (before any capacity cut), for the counters
+    misc[MISC_CMAX] = nst > misc[MISC_CMAX] ? nst : misc[MISC_CMAX];
   }
   SYNC();
 }
@@ -1945,7 +1955,16 @@ __device__ __forceinline__ double readlane(double x, int l) {
 }
 
 __device__ __forceinline__ float lane_bcast(float x, int l) { return readlane(x, l); }
-__device__ __forceinline__ double lane_bcast(double x, int l) { return __shfl(x, l); }
+#ifndef FM_F64_READLANE
+#define FM_F64_READLANE 0
+#endif
+__device__ __forceinline__ double lane_bcast(double x, int l) {
+#if FM_F64_READLANE
+  return readlane(x, l);
+#else
+  return __shfl(x, l);
+#endif
+}
 
 template <typename T>
 __device__ __forceinline__ T edge_val(const T* x3, T mu, int e);
@@ -2574,7 +2593,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     // fp32: the cost itself carries rounding noise of a few ulp of its magnitude; an "improvement" inside
     // that band is not progress (without this a stiff arena can spin to the iteration cap, and one such
     // arena sets the whole launch's duration)
-    const T noise = sizeof(T) == 4 ? T(4.8e-7) * fabs(scale * newcost) : T(0);
+    const T noise = (sizeof(T) == 4 && !(M.dbg_flags & 2)) ? T(4.8e-7) * fabs(scale * newcost) : T(0);
     cost = newcost;
     if (improvement < tol || improvement <= noise) {
       it++;
@@ -3060,7 +3079,7 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   Ws<T, DIM> w{lds_base(smem), &L};
   int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
   double* td = S.dbl + (size_t)arena * dm.dbl_stride + dm.nu;
-  int64_t* ctr = S.counters + 4 * (size_t)arena;
+  int64_t* ctr = S.counters + FM_NCTR * (size_t)arena;
   init_arena(M, w, arena);
   SYNC();
   arena_reset(M, w, arena, ti, td, ctr);
@@ -3096,10 +3115,14 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   // being hoisted out of the substep loop (which would keep every phase's addresses live everywhere)
 #define w (Ws<T, DIM>{lds_base(smem), &L})
   if (M.prof && LANE < 16) w.prof()[LANE] = LANE == PH_LAST ? wall_clock64() : 0ull;
+  if (LANE == 0) {
+    w.misc()[MISC_CSUM] = 0;
+    w.misc()[MISC_CMAX] = 0;
+  }
 #define ti (S.ints + (size_t)arena * dm.int_stride)
 #define td (S.dbl + (size_t)arena * dm.dbl_stride + nu)  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
 #define rng (S.rng + 4 * (size_t)arena)
-#define ctr (S.counters + 4 * (size_t)arena)
+#define ctr (S.counters + FM_NCTR * (size_t)arena)
 #define act (io.actions + (size_t)arena * dm.act_dim)
   // ---- ctrl_target (double) and the clipped AllFullRL control (environments.py:84-102, base_env.py:255-262)
 #define ctrl_ (w.ctrl())
@@ -3208,6 +3231,11 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
         io.scores[2 * arena + 1] = ts[I_S1];
       }
       if (io.num_obj) io.num_obj[arena] = ts[I_NIN];
+      // episode-mix counters (fm_get_counters): contacts per stage, objects in scene, episodes ended
+      ctr[4] += w.misc()[MISC_CSUM];
+      ctr[5] = w.misc()[MISC_CMAX] > ctr[5] ? w.misc()[MISC_CMAX] : ctr[5];
+      ctr[6] += ts[I_NIN];
+      ctr[7] += term;
       if (io.play_time) io.play_time[arena] = td[2];
       if (io.conveyor_speed) io.conveyor_speed[arena] = td[1];
       if (io.out_of_reach) io.out_of_reach[arena] = (uint8_t)s_fail;
@@ -3276,7 +3304,7 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const DIM dm(M.dm);
   Ws<T, DIM> w{lds_base(smem), &L};
-  int64_t* ctr = S.counters + 4 * (size_t)arena;
+  int64_t* ctr = S.counters + FM_NCTR * (size_t)arena;
   const T* ph = S.phys + (size_t)arena * dm.phys_stride;
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < dm.nu; u += WAVE) w.ctrl()[u] = dsrc[u];

@@ -50,7 +50,8 @@ class Box:
 
 class FactoryVecEnv:
     def __init__(self, num_envs, env_class="AllFullRLProgressRewardEnv", env_kwargs=None, device=0,
-                 precision="fp32", seeds=None, return_numpy=False, max_contacts=0):
+                 precision="fp32", seeds=None, return_numpy=False, max_contacts=0, solver_tolerance=0.0,
+                 solver_iterations=0):
         import torch
 
         self.torch = torch
@@ -70,6 +71,10 @@ class FactoryVecEnv:
         cfg.env_class = ENV_CLASSES[env_class]
         cfg.precision = _lib.FM_FP64 if precision == "fp64" else _lib.FM_FP32
         cfg.max_contacts = int(max_contacts)
+        if solver_tolerance > 0:  # 0 = the precision's default (fm_create)
+            cfg.solver_tolerance = float(solver_tolerance)
+        if solver_iterations > 0:
+            cfg.solver_iterations = int(solver_iterations)
         for k in ["initial_conveyor_speed", "conveyor_acceleration", "pt_time", "force_contact_threshold",
                   "control_frequency", "spawn_freq", "spawn_freq_increase", "gripper_to_closest_cube_reward_factor",
                   "closest_cube_to_bucket_reward_factor", "small_action_norm_reward_factor", "base_reward"]:
@@ -240,7 +245,7 @@ class FactoryVecEnv:
 
     def counters(self):
         self._bind_stream()
-        out = np.zeros((self.num_envs, 4), np.int64)
+        out = np.zeros((self.num_envs, 8), np.int64)
         _lib.check(self._L.fm_get_counters(self._h, out.ctypes.data_as(C.c_void_p)))
         return out
 

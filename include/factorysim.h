@@ -123,9 +123,11 @@ int fm_state_size(const fm_handle* h);                 /* bytes per arena of the
 int fm_get_state(fm_handle* h, void* host_out);        /* [N * fm_state_size] */
 int fm_set_state(fm_handle* h, const void* host_in);
 
-/* Diagnostics: per-arena counters accumulated since create (host [N*4] int64):
- * contacts dropped for capacity, Newton iterations, solver max-iteration hits, bucket-index
- * anomalies (task_utils.py:103-113 would raise IndexError). */
+/* Diagnostics: per-arena counters accumulated since create (host [N*8] int64):
+ * [0] contacts dropped for capacity, [1] Newton iterations, [2] solver max-iteration hits,
+ * [3] bucket-index anomalies (task_utils.py:103-113 would raise IndexError),
+ * [4] contacts summed over physics stages, [5] most contacts in one stage (both before any capacity
+ * cut), [6] objects in scene summed over env-steps, [7] episodes ended (terminations). */
 int fm_get_counters(fm_handle* h, int64_t* host_out);
 
 /* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [16] uint64).
@@ -137,7 +139,7 @@ int fm_profile(fm_handle* h, int mode, uint64_t* host_out);
 
 /* Diagnostic (tests only): recompute one mj_step1 + acceleration stage of `arena` at its stored stage
  * state and dump internals as float64 into host_out (capacity `cap` doubles).  Returns the number of
- * doubles written (< 0 on error).  Layout in factory_marl_amd/csrc/fm_kernel.hip (debug_kernel). */
+ * doubles written (< 0 on error).  Layout in factory_marl_amd/csrc/fm_device.hpp (debug_kernel). */
 int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int cap);
 
 #ifdef __cplusplus

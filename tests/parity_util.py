@@ -1,0 +1,103 @@
+"""Teacher-forced parity helpers shared by tests/test_gpu_parity.py and tools/parity_sweep.py (test infra).
+
+Teacher forcing: the oracle runs an episode with random AllFullRL actions; its full arena state before
+each env-step (physics stage + task layer, exported in the product's record layout) is loaded into one
+GPU arena each, every arena is stepped once with the action the oracle used, and the GPU's resulting
+state / obs / reward / flags are compared with the oracle's step.
+Metric: |dq| / max(|ref|, 1) and |dv| / max(|ref|, 0.1), the max over the arena's
+qpos / qvel; integer task state, RNG, scores, num_obj and done flags compared bit for bit.
+"""
+import numpy as np
+
+
+def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights=(0.2, 0.4, 0.1, 0.4)):
+    """oracle rollout from reset: state records before each step, actions, post-step results.
+    Episodes that terminate are reset (SB3 auto-reset), so T may span several episodes."""
+    from factory_marl_amd import state as st
+
+    rng = np.random.default_rng(seed_actions)
+    e = oracle.Env(A, K, 42, reward=reward, weights=weights)
+    e.reset()
+    recs, acts, outs = [], [], []
+    for t in range(T):
+        d, i, r = e.export_state()
+        recs.append(st.pack(A, K, d, i, r))
+        a = rng.uniform(-amp, amp, 8 * A).astype(np.float32)
+        obs, rew, term, _, info = e.step(a)
+        d2, i2, r2 = e.export_state()
+        outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
+        acts.append(a)
+        if term:
+            e.reset()
+    return np.stack(recs), np.stack(acts), outs
+
+
+def gpu_env(n, precision, A, K, env_class="AllFullRLProgressRewardEnv", **kw):
+    from factory_marl_amd import FactoryVecEnv
+
+    ekw = dict(num_arms=A, max_num_objects=K, seed=42, small_action_norm_reward_factor=0.1)
+    env = FactoryVecEnv(n, env_class=env_class, env_kwargs=ekw, precision=precision, **kw)
+    env.reset()
+    return env
+
+
+def state_err(A, K, got_dbl, ref_dbl):
+    nq, nv = 1 + 7 * K + 9 * A, 1 + 6 * K + 9 * A
+    qd = np.abs(got_dbl[:nq] - ref_dbl[:nq]) / np.maximum(np.abs(ref_dbl[:nq]), 1.0)
+    vd = np.abs(got_dbl[nq:nq + nv] - ref_dbl[nq:nq + nv]) / np.maximum(np.abs(ref_dbl[nq:nq + nv]), 0.1)
+    return qd, vd
+
+
+def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv", verbose_tol=None, **kw):
+    """one teacher-forced env-step per trajectory step, all in one launch.  Returns per-step relative state
+    errors, the steps whose integer task state / flags disagree, obs and reward errors, the counters"""
+    import torch
+
+    from factory_marl_amd import state as st
+
+    recs, acts, outs = trajectory
+    n = len(recs)
+    env = gpu_env(n, precision, A, K, env_class, **kw)
+    env.set_state(recs)
+    obs, rew, term, _ = env.step_tensors(torch.as_tensor(acts, device=env.device))
+    env.sync()
+    got = env.get_state()
+    obs, rew, term = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
+    tobs = env.terminal_obs.cpu().numpy()
+    nq = 1 + 7 * K + 9 * A
+    errs, err_steps, int_bad, flag_bad, obs_err, rew_err = [], [], [], [], [], []
+    for s in range(n):
+        o = outs[s]
+        if bool(term[s]) != o["term"]:
+            flag_bad.append(s)
+            continue
+        if o["term"]:
+            obs_err.append(np.abs(tobs[s] - o["obs"]).max())
+            continue
+        gd, gi, gr = st.unpack(A, K, got[s])
+        if not (np.array_equal(gi[:2 * K + 10], o["ints"][:2 * K + 10]) and np.array_equal(gr, o["rng"])):
+            int_bad.append(s)
+        qd, vd = state_err(A, K, gd, o["dbl"])
+        errs.append(max(qd.max(), vd.max()))
+        err_steps.append(s)
+        if verbose_tol is not None and errs[-1] > verbose_tol:
+            j = int(np.argmax(np.concatenate([qd, vd])))
+            print(f"  step {s}: worst {'qpos' if j < nq else 'qvel'}[{j if j < nq else j - nq}] "
+                  f"rel {errs[-1]:.2e} ref {o['dbl'][j]:.6g} got {gd[j]:.6g}; cubes {o['info']['num_obj']}")
+        rew_err.append(abs(rew[s] - o["reward"]))
+        obs_err.append(np.abs(obs[s] - o["obs"]).max())
+    cnt = env.counters()
+    env.close()
+    return dict(errs=np.array(errs), err_steps=np.array(err_steps, int), int_bad=int_bad, flag_bad=flag_bad,
+                obs_err=np.array(obs_err), rew_err=np.array(rew_err), counters=cnt,
+                terms=int(sum(o["term"] for o in outs)), max_cubes=max(o["info"]["num_obj"] for o in outs))
+
+
+def summary(r, gate=1e-4):
+    e = r["errs"]
+    return dict(steps=int(len(e) + len(r["flag_bad"]) + r["terms"]), compared=int(len(e)),
+                within=round(float(np.mean(e <= gate)), 4), median=float(np.median(e)), p90=float(np.quantile(e, 0.9)),
+                worst=float(e.max()), int_bad=len(r["int_bad"]), flag_bad=len(r["flag_bad"]),
+                obs_worst=float(r["obs_err"].max()), rew_worst=float(r["rew_err"].max()) if len(r["rew_err"]) else 0.0,
+                contacts_dropped=int(r["counters"][:, 0].sum()), terminations=r["terms"], max_cubes=r["max_cubes"],
+                missing_steps=[int(s) for s in r["err_steps"][e > gate]])

@@ -30,3 +30,4 @@ def test_slp_flag_only_on_fp32_objects():
     assert "-fno-slp-vectorize" not in hipflags
     assert "$(F32FLAGS)" in rules["32"]
     assert "$(F32FLAGS)" not in rules["64"] and "slp" not in rules["64"]
+    assert re.search(r"^F64FLAGS \?=\s*$", text, re.M), "fp64 objects must build with the default flags"

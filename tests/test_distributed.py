@@ -1,9 +1,10 @@
-"""Multi-GPU bench path on CPU (gloo, world size 2): each rank times its own shard of arenas, the job time
-is the slowest rank's, and the throughput counts every rank's env-steps (weak scaling, no data-path
-collective)."""
+"""Multi-rank launch path on CPU (gloo, world size 2): RankContext.from_env reads the torchrun environment and
+opens the group, each rank owns its own arena ids (weak scaling, no data-path collective), the job time is the
+slowest rank's and the throughput counts every rank's env-steps (factory_marl_amd/launch.py, bench.py)."""
 import os
 import socket
 
+import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -20,33 +21,72 @@ def _free_port():
 
 
 def _worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from factory_marl_amd import launch
+
+    ctx = launch.RankContext.from_env(use_gpu=False)
+    assert ctx.backend == "gloo" and ctx.distributed
+    lo, hi = launch.rank_arenas(4096, ctx.world, ctx.rank, "weak")
+    slo, shi = launch.rank_arenas(131072, ctx.world, ctx.rank, "strong")
+    seeds = launch.arena_seeds(lo, hi, "arena")
+    wall = 1.0 + rank  # rank 1 is the slow one
+    wmax = ctx.max_over_ranks(wall)
+    total = ctx.sum_over_ranks(hi - lo)
     import bench
 
-    wall = 1.0 + rank  # rank 1 is the slow one
-    wmax = bench.max_over_ranks(wall)
-    value = bench.job_throughput(4096, 10, world, wmax)
-    out[rank] = (wmax, value)
-    dist.barrier()
-    dist.destroy_process_group()
+    value = bench.job_throughput(hi - lo, 10, ctx.world, wmax)
+    out[rank] = (wmax, value, (lo, hi), (slo, shi), int(seeds[0]), total)
+    ctx.barrier()
+    ctx.close()
 
 
-def test_max_over_ranks_and_job_throughput_gloo():
+def test_rank_context_and_partition_gloo():
     world = 2
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
         res = dict(out)
-    assert res[0] == res[1]
-    wmax, value = res[0]
-    assert wmax == 2.0
-    assert value == pytest.approx(2 * 4096 * 10 / 2.0)
+    assert res[0][0] == res[1][0] == 2.0  # max over ranks
+    assert res[0][1] == pytest.approx(2 * 4096 * 10 / 2.0)
+    assert res[0][2] == (0, 4096) and res[1][2] == (4096, 8192)  # weak: disjoint global arena ids
+    assert res[0][3] == (0, 65536) and res[1][3] == (65536, 131072)  # config 4 split
+    assert res[0][4] == 42 and res[1][4] == 42 + 4096
+    assert res[0][5] == res[1][5] == 8192
+
+
+def test_arena_range_covers_every_arena_once():
+    from factory_marl_amd.launch import arena_range
+
+    for total, world in [(131072, 8), (32768, 8), (10, 3), (7, 7)]:
+        ids = np.concatenate([np.arange(*arena_range(total, world, r)) for r in range(world)])
+        assert np.array_equal(ids, np.arange(total))
+    with pytest.raises(ValueError):
+        arena_range(3, 4, 0)
 
 
 def test_single_rank_identity():
     import bench
+    from factory_marl_amd import launch
 
+    os.environ.pop("WORLD_SIZE", None)
+    ctx = launch.RankContext.from_env(use_gpu=False)
+    assert ctx.world == 1 and not ctx.distributed
+    assert ctx.max_over_ranks(3.5) == 3.5
     assert bench.max_over_ranks(3.5) == 3.5
     assert bench.job_throughput(4096, 10, 1, 2.0) == pytest.approx(20480.0)
+
+
+def test_bench_diagnostics_arithmetic():
+    import bench
+
+    dc = np.zeros((4, 8), np.int64)
+    dc[:, 4] = 1000  # contacts over 100 substeps x 10 steps per arena
+    dc[:, 5] = [3, 9, 4, 1]
+    dc[:, 6] = 25
+    dc[:, 7] = [0, 1, 0, 1]
+    d = bench.diagnostics(dc, 4, 10)
+    assert d["mean_contacts_per_substep"] == 1.0 and d["max_contacts_in_a_substep"] == 9
+    assert d["mean_objects_in_scene"] == 2.5 and d["episodes_ended"] == 2
+    assert bench.algorithmic_bytes(2, 4) == 120480

@@ -8,8 +8,14 @@ Tolerances: SURVEY.md §8(d) -- |dq| <= 1e-4 * max(|ref|, 1), |dv| <= 1e-4 * max
 task state, scores, num_obj, done / out_of_reach / force flags bit-exact.  The fp64 build is also held
 to 1e-7 (same algorithm, same precision as the oracle).
 """
+import os
+import sys
+
 import numpy as np
 import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import parity_util as pu  # noqa: E402
 
 torch = pytest.importorskip("torch")
 
@@ -23,24 +29,7 @@ def _have_gpu():
 
 
 def _rollout(oracle, A_, K_, T, reward="progress", seed_actions=7):
-    """oracle rollout: states before each step, actions, and the post-step results"""
-    from factory_marl_amd import state as st
-
-    rng = np.random.default_rng(seed_actions)
-    e = oracle.Env(A_, K_, 42, reward=reward, weights=(0.2, 0.4, 0.1, 0.4))
-    e.reset()
-    recs, acts, outs = [], [], []
-    for t in range(T):
-        d, i, r = e.export_state()
-        recs.append(st.pack(A_, K_, d, i, r))
-        a = rng.uniform(-2, 2, 8 * A_).astype(np.float32)
-        obs, rew, term, _, info = e.step(a)
-        d2, i2, r2 = e.export_state()
-        outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
-        acts.append(a)
-        if term:
-            e.reset()
-    return np.stack(recs), np.stack(acts), outs
+    return pu.rollout(oracle, A_, K_, T, reward=reward, seed_actions=seed_actions)
 
 
 @pytest.fixture(scope="module")
@@ -49,57 +38,13 @@ def trajectory(oracle):
 
 
 def _gpu_env(n, precision, A_=A, K_=K, env_class="AllFullRLProgressRewardEnv"):
-    from factory_marl_amd import FactoryVecEnv
-
-    kw = dict(num_arms=A_, max_num_objects=K_, seed=42, small_action_norm_reward_factor=0.1)
-    env = FactoryVecEnv(n, env_class=env_class, env_kwargs=kw, precision=precision)
-    env.reset()
-    return env
+    return pu.gpu_env(n, precision, A_, K_, env_class)
 
 
 def _compare(trajectory, precision, tol_rel, A_=A, K_=K, env_class="AllFullRLProgressRewardEnv"):
-    """returns per-step relative state errors (SURVEY metric), and the steps whose integer task state,
-    flags, obs or reward disagree"""
-    from factory_marl_amd import state as st
-
-    A, K = A_, K_
-    recs, acts, outs = trajectory
-    n = len(recs)
-    env = _gpu_env(n, precision, A, K, env_class)
-    env.set_state(recs)
-    obs, rew, term, trunc = env.step_tensors(torch.as_tensor(acts, device=env.device))
-    env.sync()
-    got = env.get_state()
-    obs = obs.cpu().numpy()
-    rew = rew.cpu().numpy()
-    term = term.cpu().numpy()
-    tobs = env.terminal_obs.cpu().numpy()
-    nq, nv, nu, nd, ni = st.sizes(A, K)
-    errs, int_bad, flag_bad, obs_err, rew_err = [], [], [], [], []
-    for s in range(n):
-        o = outs[s]
-        if bool(term[s]) != o["term"]:
-            flag_bad.append(s)
-            continue
-        if o["term"]:
-            obs_err.append(np.abs(tobs[s] - o["obs"]).max())
-            continue
-        gd, gi, gr = st.unpack(A, K, got[s])
-        if not (np.array_equal(gi[:2 * K + 10], o["ints"][:2 * K + 10]) and np.array_equal(gr, o["rng"])):
-            int_bad.append(s)
-        qd = np.abs(gd[:nq] - o["dbl"][:nq]) / np.maximum(np.abs(o["dbl"][:nq]), 1.0)
-        vd = np.abs(gd[nq:nq + nv] - o["dbl"][nq:nq + nv]) / np.maximum(np.abs(o["dbl"][nq:nq + nv]), 0.1)
-        errs.append(max(qd.max(), vd.max()))
-        if errs[-1] > 10 * tol_rel:
-            j = int(np.argmax(np.concatenate([qd, vd])))
-            print(f"  step {s}: worst {'qpos' if j < nq else 'qvel'}[{j if j < nq else j - nq}] "
-                  f"rel {errs[-1]:.2e} ref {o['dbl'][j]:.6g} got {gd[j]:.6g}; contacts {o['info'].get('ncon', '?')}")
-        rew_err.append(abs(rew[s] - o["reward"]))
-        obs_err.append(np.abs(obs[s] - o["obs"]).max())
-    cnt = env.counters()
-    env.close()
-    return dict(errs=np.array(errs), int_bad=int_bad, flag_bad=flag_bad, obs_err=np.array(obs_err),
-                rew_err=np.array(rew_err), counters=cnt, tol=tol_rel)
+    r = pu.compare(trajectory, precision, A_, K_, env_class, verbose_tol=10 * tol_rel)
+    r["tol"] = tol_rel
+    return r
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")

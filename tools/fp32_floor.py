@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Inherent fp32 floor of the SURVEY parity gate (CPU only, oracle = checker).
+
+The fp32 GPU arena stores its physics state in float32, so a teacher-forced fp32 step starts from the
+oracle's float64 state ROUNDED to float32 (~6e-8 relative).  This tool steps the float64 oracle itself from
+that rounded state and compares with the unrounded step, with the SURVEY §8(d) metric
+|d| <= 1e-4 * max(|ref|, s) (s = 1 for qpos, 0.1 for qvel).  A step that misses the gate here misses it for
+ANY fp32-state implementation of the algorithm: the miss is inherent (input rounding amplified by the
+step's contact events), not the kernel's arithmetic.
+
+usage: python tools/fp32_floor.py [A K T seed_actions] [--json out.json]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import pyoracle as po  # noqa: E402  (test infrastructure)
+
+
+def rel_err(A, K, got, ref):
+    nq, nv = 1 + 7 * K + 9 * A, 1 + 6 * K + 9 * A
+    qd = np.abs(got[:nq] - ref[:nq]) / np.maximum(np.abs(ref[:nq]), 1.0)
+    vd = np.abs(got[nq:nq + nv] - ref[nq:nq + nv]) / np.maximum(np.abs(ref[nq:nq + nv]), 0.1)
+    return float(max(qd.max(), vd.max()))
+
+
+def floor_study(A, K, T, seed_actions=7, amp=1.0, rng_perturb=None):
+    """returns per-step (rel err of the rounded-start step vs the exact step, terminated, flag flips)"""
+    nq, nv = 1 + 7 * K + 9 * A, 1 + 6 * K + 9 * A
+    nphys = 2 * nq + 3 * nv
+    rng = np.random.default_rng(seed_actions)
+    e = po.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4))
+    e.reset()
+    p = po.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4))
+    p.reset()
+    out = []
+    for t in range(T):
+        d, i, r = e.export_state()
+        a = rng.uniform(-2, 2, 8 * A).astype(np.float32)
+        dp = d.copy()
+        if rng_perturb is None:
+            dp[:nphys] = dp[:nphys].astype(np.float32).astype(np.float64)
+        else:  # random relative perturbation of amplitude amp * 2^-24 (float32 half-ulp scale)
+            dp[:nphys] *= 1 + amp * 2.0 ** -24 * rng_perturb.uniform(-1, 1, nphys)
+        p.import_state(dp, i, r)
+        _, _, term, _, info = e.step(a)
+        _, _, pterm, _, pinfo = p.step(a)
+        d2, i2, _ = e.export_state()
+        p2, pi2, _ = p.export_state()
+        flip = (term != pterm) or not np.array_equal(i2, pi2)
+        out.append(dict(step=t, err=None if term else rel_err(A, K, p2, d2), term=bool(term), flip=bool(flip),
+                        ncubes=int(info["num_obj"])))
+        if term:
+            e.reset()
+    return out
+
+
+def summarize(rows, gate=1e-4):
+    e = np.array([r["err"] for r in rows if r["err"] is not None])
+    return dict(steps=len(rows), compared=len(e), within=float(np.mean(e <= gate)), median=float(np.median(e)),
+                worst=float(e.max()), flips=sum(r["flip"] for r in rows),
+                missing_steps=[r["step"] for r in rows if r["err"] is not None and r["err"] > gate])
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    A, K, T, sa = (int(x) for x in (args + ["2", "4", "96", "7"][len(args):]))
+    po.build()
+    rows = floor_study(A, K, T, sa)
+    s = summarize(rows)
+    print(json.dumps(dict(A=A, K=K, T=T, seed_actions=sa, **s)))
+    if "--json" in sys.argv:
+        json.dump(dict(summary=s, rows=rows), open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)

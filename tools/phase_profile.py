@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root (bench, package)
 
 
 def main():
@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--arenas", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--preroll", type=int, default=200, help="desynchronising pre-roll (bench.preroll)")
     args = ap.parse_args()
     import torch
 
@@ -25,6 +26,9 @@ def main():
     env = FactoryVecEnv(args.arenas, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42),
                         precision=args.precision)
     env.reset()
+    import bench
+
+    bench.preroll(env, args.preroll, 0, env.device)
     g = torch.Generator(device=env.device)
     g.manual_seed(0)
     for _ in range(5):
@@ -44,6 +48,8 @@ def main():
     rep["_mean_ncon"] = round(ncon / sub, 3)
     rep["_lds_bytes_per_arena"] = env._L.fm_workspace_bytes(env._h)
     rep["_newton_iters_per_substep"] = round(float(c1[1] - c0[1]) / sub, 3)
+    rep["_mean_objects_in_scene"] = round(float(c1[6] - c0[6]) / (args.arenas * args.steps), 3)
+    rep["_preroll"] = args.preroll
     print(json.dumps(rep, indent=1))
 
 

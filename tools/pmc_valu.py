@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""VALU work of the env-step kernel per arena env-step from one rocprofv3 --pmc pass (test/measurement infra).
+
+usage: python tools/pmc_valu.py PMC.csv --arenas 4096 --last 3 [--precision fp32] [--out profiles/pmc_valu.json]
+Counters (one pass, 8 SQ slots): SQ_INSTS_VALU, SQ_INSTS_VALU_ADD_F32, SQ_INSTS_VALU_MUL_F32, SQ_INSTS_VALU_FMA_F32,
+SQ_INSTS_VALU_TRANS_F32, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAVES.  Instruction counters count wave-instructions:
+lane FLOPs = 64 x (ADD + MUL + TRANS + 2 FMA) -- every lane of the wave, active or not, so an upper bound on the
+useful fp32 FLOPs.  Only the last `--last` step_kernel dispatches are used (the timed steps after the pre-roll).
+"""
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--arenas", type=int, default=4096)
+    ap.add_argument("--last", type=int, default=3)
+    ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--arms", type=int, default=2)
+    ap.add_argument("--objects", type=int, default=4)
+    ap.add_argument("--out", default="profiles/pmc_valu.json")
+    a = ap.parse_args()
+    per = defaultdict(dict)
+    for r in csv.DictReader(open(a.csv)):
+        if "step_kernel" not in r["Kernel_Name"]:
+            continue
+        key = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+        per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    keys = sorted(per)[-a.last:]
+    tot = defaultdict(float)
+    for k in keys:
+        for c, v in per[k].items():
+            tot[c] += v / len(keys)
+    n = a.arenas
+    f = "F32" if a.precision == "fp32" else "F64"
+    flop = 64.0 * (tot.get(f"SQ_INSTS_VALU_ADD_{f}", 0) + tot.get(f"SQ_INSTS_VALU_MUL_{f}", 0) +
+                   tot.get(f"SQ_INSTS_VALU_TRANS_{f}", 0) + 2 * tot.get(f"SQ_INSTS_VALU_FMA_{f}", 0))
+    rec = {"kernel": "fm::step_kernel", "arenas": n, "precision": a.precision, "A": a.arms, "K": a.objects,
+           "dispatches": len(keys), "counters_per_launch": dict(tot),
+           "valu_wave_instr_per_arena_step": tot.get("SQ_INSTS_VALU", 0) / n,
+           "valu_lane_flops_per_arena_step": flop / n,
+           "note": "mean over the last dispatches; lane FLOPs count all 64 lanes of each executed wave-instruction"}
+    with open(a.out, "w") as fo:
+        json.dump(rec, fo, indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
