@@ -155,7 +155,7 @@ static Model<T> make_model(const fm_handle* h) {
 template <typename T>
 static State<T> make_state(const fm_handle* h) {
   State<T> S;
-  S.phys = (T*)h->phys;
+  S.phys = (double*)h->phys;
   S.dbl = h->dbl;
   S.ints = h->ints;
   S.rng = h->rng;
@@ -259,9 +259,10 @@ static int create_typed(fm_handle* h) {
   if ((r = upload_raw<uint32_t>(h, &h->tri, s.tri))) return r;
   // state
   size_t N = d.N;
-  HIPCHK(hipMalloc(&h->phys, N * d.phys_stride * sizeof(T)));
+  // the physics state is float64 in both precisions (fp32 computes from float copies of it)
+  HIPCHK(hipMalloc(&h->phys, N * d.phys_stride * sizeof(double)));
   h->allocs.push_back(h->phys);
-  HIPCHK(hipMemset(h->phys, 0, N * d.phys_stride * sizeof(T)));
+  HIPCHK(hipMemset(h->phys, 0, N * d.phys_stride * sizeof(double)));
   HIPCHK(hipMalloc((void**)&h->dbl, N * d.dbl_stride * sizeof(double)));
   h->allocs.push_back(h->dbl);
   HIPCHK(hipMemset(h->dbl, 0, N * d.dbl_stride * sizeof(double)));
@@ -307,12 +308,12 @@ template <typename T>
 static int get_state_typed(fm_handle* h, char* out) {
   const Dims& d = h->dm;
   size_t N = d.N;
-  std::vector<T> ph(N * d.phys_stride);
+  std::vector<double> ph(N * d.phys_stride);
   std::vector<double> db(N * d.dbl_stride);
   std::vector<int32_t> in(N * d.int_stride);
   std::vector<uint64_t> rg(N * 4);
   HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(ph.data(), h->phys, ph.size() * sizeof(T), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ph.data(), h->phys, ph.size() * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(db.data(), h->dbl, db.size() * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(in.data(), h->ints, in.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(rg.data(), h->rng, rg.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -320,7 +321,7 @@ static int get_state_typed(fm_handle* h, char* out) {
   for (size_t n = 0; n < N; n++) {
     char* o = out + n * rec;
     double* dp = (double*)o;
-    for (int i = 0; i < d.phys_stride; i++) dp[i] = (double)ph[n * d.phys_stride + i];
+    for (int i = 0; i < d.phys_stride; i++) dp[i] = ph[n * d.phys_stride + i];
     for (int i = 0; i < d.dbl_stride; i++) dp[d.phys_stride + i] = db[n * d.dbl_stride + i];
     int32_t* ip = (int32_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double));
     for (int i = 0; i < d.int_stride; i++) ip[i] = in[n * d.int_stride + i];
@@ -334,7 +335,7 @@ template <typename T>
 static int set_state_typed(fm_handle* h, const char* src) {
   const Dims& d = h->dm;
   size_t N = d.N;
-  std::vector<T> ph(N * d.phys_stride);
+  std::vector<double> ph(N * d.phys_stride);
   std::vector<double> db(N * d.dbl_stride);
   std::vector<int32_t> in(N * d.int_stride);
   std::vector<uint64_t> rg(N * 4);
@@ -342,7 +343,7 @@ static int set_state_typed(fm_handle* h, const char* src) {
   for (size_t n = 0; n < N; n++) {
     const char* o = src + n * rec;
     const double* dp = (const double*)o;
-    for (int i = 0; i < d.phys_stride; i++) ph[n * d.phys_stride + i] = (T)dp[i];
+    for (int i = 0; i < d.phys_stride; i++) ph[n * d.phys_stride + i] = dp[i];
     for (int i = 0; i < d.dbl_stride; i++) db[n * d.dbl_stride + i] = dp[d.phys_stride + i];
     const int32_t* ip = (const int32_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double));
     for (int i = 0; i < d.int_stride; i++) in[n * d.int_stride + i] = ip[i];
@@ -351,7 +352,7 @@ static int set_state_typed(fm_handle* h, const char* src) {
     for (int i = 0; i < 4; i++) rg[n * 4 + i] = up[i];
   }
   HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(h->phys, ph.data(), ph.size() * sizeof(T), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->phys, ph.data(), ph.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->rng, rg.data(), rg.size() * sizeof(uint64_t), hipMemcpyHostToDevice));

@@ -58,7 +58,7 @@ struct Dims {
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
-  int phys_stride;  // T:      qpos nq | qvel nv | qpos_s nq | qvel_s nv | qacc_ws nv
+  int phys_stride;  // double: qpos nq | qvel nv | qpos_s nq | qvel_s nv | qacc_ws nv
   int dbl_stride;   // double: ctrl_target nu | spawn_freq | speed | play_time | last_grip A | last_bucket A | ep_return
   int int_stride;   // int32:  in_scene K | out_scene K | n_in n_out step since fail hidden score0 score1 last0 last1 ep_len
 };
@@ -104,7 +104,7 @@ struct Model {
 
 template <typename T>
 struct State {
-  gptr<T> phys;
+  gptr<double> phys;  // float64 in both builds (the fp32 physics keeps a float64 master state)
   gptr<double> dbl;
   gptr<int32_t> ints;
   gptr<uint64_t> rng;      // [N][4]
@@ -161,8 +161,9 @@ __device__ __forceinline__ char* lds_base(char* smem) {
 // byte offsets of the per-arena LDS workspace (computed on the host, see lds_layout())
 struct Lay {
   int q, v, a, as, fs, fc, pb, g, dir, Ma, tmp, fa;
+  int qd, vd;  // double master copies of q / v (fp32 build; the same arrays as q / v in fp64)
   int ctrl;   // double
-  int alen, avel, aforce;
+  int aforce;
   int bpos, bR, bcom, bIw, bF, bN, dax, danc, site;
   int cR;
   int Marm;
@@ -364,9 +365,11 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.Ma = take(tsize * nv);
   L.tmp = take(tsize * nv);
   L.fa = take(tsize * nv);
+  // float64 master state: the fp32 physics reads the float copies q / v, the integrator accumulates in
+  // double (an fp32 qpos cannot absorb increments below half an ulp: dt * qvel of a joint at rest)
+  L.qd = tsize == 8 ? L.q : take(8 * nq);
+  L.vd = tsize == 8 ? L.v : take(8 * nv);
   L.ctrl = take(8 * nu);
-  L.alen = take(tsize * nu);
-  L.avel = take(tsize * nu);
   L.aforce = take(tsize * nu);
   L.bpos = take(tsize * 30 * A);
   L.bR = take(tsize * 90 * A);

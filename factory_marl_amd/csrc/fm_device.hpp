@@ -174,20 +174,20 @@ struct Ws {
       return (double*)(base + L->ctrl);
     }
   }
-  __device__ __forceinline__ T* alen() const {
+  __device__ __forceinline__ double* qd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.alen);
+      return (double*)(base + c.qd);
     } else {
-      return (T*)(base + L->alen);
+      return (double*)(base + L->qd);
     }
   }
-  __device__ __forceinline__ T* avel() const {
+  __device__ __forceinline__ double* vd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.avel);
+      return (double*)(base + c.vd);
     } else {
-      return (T*)(base + L->avel);
+      return (double*)(base + L->vd);
     }
   }
   __device__ __forceinline__ T* aforce() const {
@@ -1581,26 +1581,6 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   if (LANE < A) arm_rne_back(M, w, LANE);
   SYNC();
   PMARK(PH_FK);
-  // ---- actuator length / velocity (transmission at the stage state)
-  for (int u = LANE; u < dm.nu; u += WAVE) {
-    T L, V;
-    if (u == 0) {
-      L = q[0];
-      V = v[0];
-    } else {
-      int arm = (u - 1) / 8, j = (u - 1) % 8;
-      int qa = 1 + 7 * K + 9 * arm, va = 1 + 6 * K + 9 * arm;
-      if (j < 7) {
-        L = q[qa + j];
-        V = v[va + j];
-      } else {
-        L = T(0.5) * q[qa + 7] + T(0.5) * q[qa + 8];
-        V = T(0.5) * v[va + 7] + T(0.5) * v[va + 8];
-      }
-    }
-    w.alen()[u] = L;
-    w.avel()[u] = V;
-  }
   // ---- arm mass-matrix blocks, composite-rigid-body style.  Hinge i moves the bodies b >= i; about its anchor
   // p_i their composite mass moment h_i = sum m r and inertia J_i = sum Iw + m (|r|^2 1 - r r'), r = com - p_i
   // (one lane per hinge; the Hessian region is free before the collision).  Then one entry (i >= j) per lane:
@@ -2628,28 +2608,46 @@ __device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T, DIM>& 
   for (int i = LANE; i < nv; i += WAVE) fa[i] = T(0);
   SYNC();
   if (actuation) {
+    // actuator forces in float64 (MuJoCo's gain * ctrl + bias, base_env.py:217 ctrl is float64): the PD
+    // difference ctrl - length is exact, only the force is rounded to the build's precision
     for (int u = LANE; u < dm.nu; u += WAVE) {
-      T c = (T)w.ctrl()[u];
-      T lo = M.ctrlrange[2 * u], hi = M.ctrlrange[2 * u + 1];
+      double c = w.ctrl()[u];
+      const double lo = (double)M.ctrlrange[2 * u], hi = (double)M.ctrlrange[2 * u + 1];
       c = c < lo ? lo : (c > hi ? hi : c);
-      T L = w.alen()[u], V = w.avel()[u];
+      // transmission (actuator length / velocity) from the float64 master state: the belt and arm dofs it
+      // reads are the stage state's (the TaskManager's teleports only move cubes)
+      double L, V;
       if (u == 0) {
-        T f = M.belt_kv * c - M.belt_kv * V;
+        L = w.qd()[0];
+        V = w.vd()[0];
+      } else {
+        const int qa = 1 + 7 * K + 9 * ((u - 1) / 8), va = 1 + 6 * K + 9 * ((u - 1) / 8), jj = (u - 1) % 8;
+        if (jj < 7) {
+          L = w.qd()[qa + jj];
+          V = w.vd()[va + jj];
+        } else {
+          L = 0.5 * w.qd()[qa + 7] + 0.5 * w.qd()[qa + 8];
+          V = 0.5 * w.vd()[va + 7] + 0.5 * w.vd()[va + 8];
+        }
+      }
+      if (u == 0) {
+        const double kv = (double)M.belt_kv;
+        const T f = (T)(kv * c - kv * V);
         w.aforce()[u] = f;
         fa[0] = f;
       } else {
         int arm = (u - 1) / 8, j = (u - 1) % 8;
         int va = 1 + 6 * K + 9 * arm;
         if (j < 7) {
-          T f = T(2000) * c + T(-2000) * L + T(-200) * V;
+          const T f = (T)(2000.0 * c + -2000.0 * L + -200.0 * V);
           w.aforce()[u] = f;
           fa[va + j] = f;
         } else {
-          T f = T(100) * c + T(-100) * L + T(-10) * V;
-          f = f < T(-100) ? T(-100) : (f > T(100) ? T(100) : f);
-          w.aforce()[u] = f;
-          fa[va + 7] = T(0.5) * f;
-          fa[va + 8] = T(0.5) * f;
+          double f = 100.0 * c + -100.0 * L + -10.0 * V;
+          f = f < -100.0 ? -100.0 : (f > 100.0 ? 100.0 : f);
+          w.aforce()[u] = (T)f;
+          fa[va + 7] = (T)(0.5 * f);
+          fa[va + 8] = (T)(0.5 * f);
         }
       }
     }
@@ -2716,49 +2714,64 @@ __device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T
     for (int k = 0; k < 9; k++) acc[a0 + 9 * LANE + k] = x[k];
   }
   SYNC();
-  for (int i = LANE; i < nv; i += WAVE) v[i] += dt * acc[i];
+  // velocities and positions accumulate in the float64 master state (mj_integratePos); the float copies
+  // the fp32 physics reads are refreshed from it
+  double* qd = w.qd();
+  double* vd = w.vd();
+  const double h = 0.001;  // model.opt.timestep (base_env.py:207-210), exact in float64
+  for (int i = LANE; i < nv; i += WAVE) {
+    vd[i] += h * (double)acc[i];
+    if constexpr (sizeof(T) != 8) v[i] = (T)vd[i];
+  }
   SYNC();
-  // positions with the new velocities (mj_integratePos)
-  if (LANE == 0) q[0] += dt * v[0];
+  if (LANE == 0) {
+    qd[0] += h * vd[0];
+    if constexpr (sizeof(T) != 8) q[0] = (T)qd[0];
+  }
   for (int k = LANE; k < K; k += WAVE) {
-    T* qq = q + 1 + 7 * k;
-    const T* vv = v + 1 + 6 * k;
-    for (int c = 0; c < 3; c++) qq[c] += dt * vv[c];
-    T ax[3] = {vv[3], vv[4], vv[5]};
-    T nrm = sqrt(dot3(ax, ax));
-    if (nrm < T(1e-15)) {
+    double* qq = qd + 1 + 7 * k;
+    const double* vv = vd + 1 + 6 * k;
+    for (int c = 0; c < 3; c++) qq[c] += h * vv[c];
+    double ax[3] = {vv[3], vv[4], vv[5]};
+    double nrm = sqrt(dot3(ax, ax));
+    if (nrm < 1e-15) {
       ax[0] = 1;
       ax[1] = ax[2] = 0;
     } else {
       for (int c = 0; c < 3; c++) ax[c] /= nrm;
     }
-    T ang = dt * nrm;
-    T qr[4];
-    if (ang == T(0)) {
+    double ang = h * nrm;
+    double qr[4];
+    if (ang == 0.0) {
       qr[0] = 1;
       qr[1] = qr[2] = qr[3] = 0;
     } else {
-      T s = sin(ang * T(0.5));
-      qr[0] = cos(ang * T(0.5));
+      double s = sin(ang * 0.5);
+      qr[0] = cos(ang * 0.5);
       qr[1] = ax[0] * s;
       qr[2] = ax[1] * s;
       qr[3] = ax[2] * s;
     }
-    T qu[4] = {qq[3], qq[4], qq[5], qq[6]};
-    T n = sqrt(qu[0] * qu[0] + qu[1] * qu[1] + qu[2] * qu[2] + qu[3] * qu[3]);
-    if (n < T(1e-15)) {
+    double qu[4] = {qq[3], qq[4], qq[5], qq[6]};
+    double n = sqrt(qu[0] * qu[0] + qu[1] * qu[1] + qu[2] * qu[2] + qu[3] * qu[3]);
+    if (n < 1e-15) {
       qu[0] = 1;
       qu[1] = qu[2] = qu[3] = 0;
-    } else if (fabs(n - T(1)) > T(1e-15)) {
+    } else if (fabs(n - 1.0) > 1e-15) {
       for (int c = 0; c < 4; c++) qu[c] /= n;
     }
     qq[3] = qu[0] * qr[0] - qu[1] * qr[1] - qu[2] * qr[2] - qu[3] * qr[3];
     qq[4] = qu[0] * qr[1] + qu[1] * qr[0] + qu[2] * qr[3] - qu[3] * qr[2];
     qq[5] = qu[0] * qr[2] - qu[1] * qr[3] + qu[2] * qr[0] + qu[3] * qr[1];
     qq[6] = qu[0] * qr[3] + qu[1] * qr[2] - qu[2] * qr[1] + qu[3] * qr[0];
+    if constexpr (sizeof(T) != 8)
+      for (int c = 0; c < 7; c++) q[1 + 7 * k + c] = (T)qq[c];
   }
   int qa0 = 1 + 7 * K;
-  for (int i = LANE; i < 9 * dm.A; i += WAVE) q[qa0 + i] += dt * v[a0 + i];
+  for (int i = LANE; i < 9 * dm.A; i += WAVE) {
+    qd[qa0 + i] += h * vd[a0 + i];
+    if constexpr (sizeof(T) != 8) q[qa0 + i] = (T)qd[qa0 + i];
+  }
   SYNC();
   PMARK(PH_INT);
 }
@@ -2784,18 +2797,18 @@ __device__ __forceinline__ double pcg_double(uint64_t* st) {
   return (double)(pcg_next(st) >> 11) * (1.0 / 9007199254740992.0);
 }
 
-template <typename T, typename DD>
-__device__ __forceinline__ void hide_cube(const DD& dm, T* q, T* v, int32_t* ti, int obj) {
+template <typename DD>
+__device__ __forceinline__ void hide_cube(const DD& dm, double* q, double* v, int32_t* ti, int obj) {
   ti[dm.K + ti[2 * dm.K + I_NOUT]] = obj;
   ti[2 * dm.K + I_NOUT]++;
-  T* qq = q + 1 + 7 * obj;
-  qq[0] = T(4.0 + 1.0);
-  qq[1] = T(ti[2 * dm.K + I_HIDDEN] * 0.2);
-  qq[2] = T(1.0);
-  qq[3] = T(1.0);
-  qq[4] = qq[5] = qq[6] = T(0);
-  T* vv = v + 1 + 6 * obj;
-  for (int k = 0; k < 6; k++) vv[k] = T(0);
+  double* qq = q + 1 + 7 * obj;
+  qq[0] = 4.0 + 1.0;
+  qq[1] = ti[2 * dm.K + I_HIDDEN] * 0.2;
+  qq[2] = 1.0;
+  qq[3] = 1.0;
+  qq[4] = qq[5] = qq[6] = 0.0;
+  double* vv = v + 1 + 6 * obj;
+  for (int k = 0; k < 6; k++) vv[k] = 0.0;
   ti[2 * dm.K + I_HIDDEN]++;
 }
 
@@ -2807,18 +2820,18 @@ __device__ __forceinline__ void pop_at(int32_t* list, int32_t* n, int idx) {
 
 // TaskManager.reset (task_utils.py:146-156) + BaseEnv.reset_sim bits (base_env.py:184-190)
 template <typename T, typename DIM>
-__device__ __forceinline__ void task_reset(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, double* ctrl) {
+__device__ __forceinline__ void task_reset(const Model<T>& M, double* q, double* v, int32_t* ti, double* td, double* ctrl) {
   const DIM dm(M.dm);
   const int K = dm.K;
   for (int k = 0; k < K; k++) {
-    T* qq = q + 1 + 7 * k;
-    qq[0] = T(4.0);
-    qq[1] = T(0.0 + k * 0.2);
-    qq[2] = T(1.0);
-    qq[3] = T(1.0);
-    qq[4] = qq[5] = qq[6] = T(0);
-    T* vv = v + 1 + 6 * k;
-    for (int c = 0; c < 6; c++) vv[c] = T(0);
+    double* qq = q + 1 + 7 * k;
+    qq[0] = 4.0;
+    qq[1] = 0.0 + k * 0.2;
+    qq[2] = 1.0;
+    qq[3] = 1.0;
+    qq[4] = qq[5] = qq[6] = 0.0;
+    double* vv = v + 1 + 6 * k;
+    for (int c = 0; c < 6; c++) vv[c] = 0.0;
     ti[K + k] = k;
     ti[k] = -1;
   }
@@ -2835,7 +2848,7 @@ __device__ __forceinline__ void task_reset(const Model<T>& M, T* q, T* v, int32_
 }
 
 template <typename T, typename DIM>
-__device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr,
+__device__ __forceinline__ int task_step(const Model<T>& M, double* q, double* v, int32_t* ti, double* td, uint64_t* rng, int64_t* ctr,
                                          int* orig) {
   const DIM dm(M.dm);
   const int K = dm.K;
@@ -2847,11 +2860,11 @@ __device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t*
     if (ts[I_NOUT] > 0) {
       int obj = outs[0];
       pop_at(outs, &ts[I_NOUT], 0);
-      T* qq = q + 1 + 7 * obj;
-      qq[0] = T(0.0);
-      qq[1] = T(1.0);
-      qq[2] = T(2.0);
-      for (int k = 0; k < 4; k++) qq[3 + k] = T(0.0 + 1.0 * pcg_double(rng));
+      double* qq = q + 1 + 7 * obj;
+      qq[0] = 0.0;
+      qq[1] = 1.0;
+      qq[2] = 2.0;
+      for (int k = 0; k < 4; k++) qq[3 + k] = 0.0 + 1.0 * pcg_double(rng);
       ins[ts[I_NIN]++] = obj;
     }
     ts[I_SINCE] = 0;
@@ -2860,8 +2873,8 @@ __device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t*
     // out of bounds (task_utils.py:84-94): popping index i only shifts the entries above i, which the
     // descending walk has already visited, so each test reads the position it would have read up front
     for (int i = ts[I_NIN] - 1; i >= 0; i--) {
-      const T* qq = q + 1 + 7 * ins[i];
-      const double x = (double)qq[0], y = (double)qq[1], z = (double)qq[2];
+      const double* qq = q + 1 + 7 * ins[i];
+      const double x = qq[0], y = qq[1], z = qq[2];
       if (!(fabs(x) > 1.2 || y < -1.5 || z < 0.9)) continue;
       int obj = ins[i];
       pop_at(ins, &ts[I_NIN], i);
@@ -2878,10 +2891,10 @@ __device__ __forceinline__ int task_step(const Model<T>& M, T* q, T* v, int32_t*
       for (int b = 0; b < 2; b++) {
         double bx = b == 0 ? M.bucket_x0 : M.bucket_x1, by = M.bucket_y, bz = M.bucket_z;
         for (int i = n2 - 1; i >= 0; i--) {
-          const T* qq = q + 1 + 7 * orig[i];
-          bool in_x = fabs((double)qq[0] - bx) <= 0.6 * 0.29;
-          bool in_y = fabs((double)qq[1] - by) <= 0.6 * 0.29;
-          bool in_z = (double)qq[2] - bz - 0.02 / 2 <= 0.07;
+          const double* qq = q + 1 + 7 * orig[i];
+          bool in_x = fabs(qq[0] - bx) <= 0.6 * 0.29;
+          bool in_y = fabs(qq[1] - by) <= 0.6 * 0.29;
+          bool in_z = qq[2] - bz - 0.02 / 2 <= 0.07;
           if (!(in_x && in_y && in_z)) continue;
           if (i >= ts[I_NIN]) {  // reference: IndexError (task_utils.py:103-113 index reuse)
             ctr[3] += 1;
@@ -2910,7 +2923,7 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
   double* sc = w.scal();
-  int fail = task_step<T, DIM>(M, w.q(), w.v(), ti, td, rng, ctr, w.sortidx());
+  int fail = task_step<T, DIM>(M, w.qd(), w.vd(), ti, td, rng, ctr, w.sortidx());
   double dt_env = 0.001 * dm.frame_skip;
   td[2] += dt_env;
   td[1] += M.accel * dt_env;
@@ -2930,9 +2943,8 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
       double best = 0;
       int bi = -1;
       for (int c = 0; c < ts[I_NIN]; c++) {
-        const T* qq = w.q() + 1 + 7 * ti[c];
-        double dx = (double)qq[0] - (double)gp[0], dy = (double)qq[1] - (double)gp[1],
-               dz = (double)qq[2] - (double)gp[2];
+        const double* qq = w.qd() + 1 + 7 * ti[c];
+        double dx = qq[0] - (double)gp[0], dy = qq[1] - (double)gp[1], dz = qq[2] - (double)gp[2];
         double dd = sqrt(dx * dx + dy * dy + dz * dz);
         if (bi < 0 || dd < best) {
           best = dd;
@@ -2942,9 +2954,9 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
       gc += lg[i] - best;
       lg[i] = best;
       // closest cube to this arm's bucket
-      const T* qq = w.q() + 1 + 7 * ti[bi];
+      const double* qq = w.qd() + 1 + 7 * ti[bi];
       double bx = (i % 2) == 0 ? M.bucket_x0 : M.bucket_x1;
-      double dx = (double)qq[0] - bx, dy = (double)qq[1] - M.bucket_y, dz = (double)qq[2] - M.bucket_z;
+      double dx = qq[0] - bx, dy = qq[1] - M.bucket_y, dz = qq[2] - M.bucket_z;
       double db = sqrt(dx * dx + dy * dy + dz * dz);
       bc += lb[i] - db;
       lb[i] = db;
@@ -2969,15 +2981,15 @@ template <typename T, typename DIM>
 __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w, const int32_t* ti, float* obs) {
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
-  const T* q = w.q();
-  const T* v = w.v();
+  const double* q = w.qd();  // float64 state cast to float32 (base_env.py:92-109)
+  const double* v = w.vd();
   int* idx = w.sortidx();
   if (LANE == 0) {
     int n = ti[2 * K + I_NIN];
     for (int i = 0; i < n; i++) idx[i] = ti[i];
     for (int i = 1; i < n; i++) {
       int vi = idx[i];
-      T x = q[1 + 7 * vi];
+      double x = q[1 + 7 * vi];
       int j = i - 1;
       while (j >= 0 && q[1 + 7 * idx[j]] > x) {
         idx[j + 1] = idx[j];
@@ -3012,14 +3024,25 @@ __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w
 // ------------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------------
+// float copies of the float64 master state (fp32 build; in fp64 they are the same arrays)
+template <typename T, typename DIM>
+__device__ __forceinline__ void refresh_copies(const Model<T>& M, const Ws<T, DIM>& w) {
+  if constexpr (sizeof(T) != 8) {
+    const DIM dm(M.dm);
+    for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = (T)w.qd()[i];
+    for (int i = LANE; i < dm.nv; i += WAVE) w.v()[i] = (T)w.vd()[i];
+  }
+}
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void load_state(const Model<T>& M, const State<T>& S, const Ws<T, DIM>& w, int arena, bool stage_copy) {
   const DIM dm(M.dm);
-  const T* ph = S.phys + (size_t)arena * dm.phys_stride;
-  const T* src_q = ph + (stage_copy ? dm.nq + dm.nv : 0);
-  const T* src_v = ph + dm.nq + (stage_copy ? dm.nq + dm.nv : 0);
-  for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = src_q[i];
-  for (int i = LANE; i < dm.nv; i += WAVE) w.v()[i] = src_v[i];
+  const double* ph = S.phys + (size_t)arena * dm.phys_stride;
+  const double* src_q = ph + (stage_copy ? dm.nq + dm.nv : 0);
+  const double* src_v = ph + dm.nq + (stage_copy ? dm.nq + dm.nv : 0);
+  for (int i = LANE; i < dm.nq; i += WAVE) w.qd()[i] = src_q[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) w.vd()[i] = src_v[i];
+  refresh_copies(M, w);
 }
 
 // per-launch LDS setup: geom / collision-body tables, static geom centres, body bounds, cube sizes
@@ -3038,16 +3061,18 @@ __device__ __forceinline__ void init_arena(const Model<T>& M, const Ws<T, DIM>& 
 template <typename T, typename DIM>
 __device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T, DIM>& w, int arena, int32_t* ti, double* td, int64_t* ctr) {
   const DIM dm(M.dm);
-  T* q = w.q();
-  T* v = w.v();
-  for (int i = LANE; i < dm.nq; i += WAVE) q[i] = T(0);
+  double* q = w.qd();
+  double* v = w.vd();
+  for (int i = LANE; i < dm.nq; i += WAVE) q[i] = 0.0;
   for (int i = LANE; i < dm.nv; i += WAVE) {
-    v[i] = T(0);
+    v[i] = 0.0;
     w.a()[i] = T(0);
   }
   SYNC();
   if (LANE == 0) task_reset<T, DIM>(M, q, v, ti, td, w.ctrl());
   FULL_SYNC();
+  SYNC();
+  refresh_copies(M, w);
   SYNC();
   stage(M, w, arena, ctr);
   smooth_acc(M, w, arena, false);
@@ -3062,10 +3087,10 @@ __device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T, DIM>&
 template <typename T, typename DIM>
 __device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S, const Ws<T, DIM>& w, int arena) {
   const DIM dm(M.dm);
-  T* ph = S.phys + (size_t)arena * dm.phys_stride;
-  for (int i = LANE; i < dm.nq; i += WAVE) ph[i] = w.q()[i];
-  for (int i = LANE; i < dm.nv; i += WAVE) ph[dm.nq + i] = w.v()[i];
-  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + 2 * dm.nv + i] = w.a()[i];
+  double* ph = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nq; i += WAVE) ph[i] = w.qd()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[dm.nq + i] = w.vd()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + 2 * dm.nv + i] = (double)w.a()[i];
   double* db = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < dm.nu; u += WAVE) db[u] = w.ctrl()[u];
 }
@@ -3084,9 +3109,9 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   SYNC();
   arena_reset(M, w, arena, ti, td, ctr);
   // stage state = reset state
-  T* ph = S.phys + (size_t)arena * dm.phys_stride;
-  for (int i = LANE; i < dm.nq; i += WAVE) ph[dm.nq + dm.nv + i] = w.q()[i];
-  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + dm.nv + i] = w.v()[i];
+  double* ph = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nq; i += WAVE) ph[dm.nq + dm.nv + i] = w.qd()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + dm.nv + i] = w.vd()[i];
   store_state(M, S, w, arena);
   if (LANE == 0) {
     td[2 * dm.A + 3] = 0.0;  // episode return
@@ -3146,8 +3171,8 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   }
   init_arena(M, w, arena);
   // warmstart
-  const T* ph = S.phys + (size_t)arena * dm.phys_stride;
-  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
+  const double* ph = S.phys + (size_t)arena * dm.phys_stride;
+  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = (T)ph[2 * dm.nq + 2 * dm.nv + i];
   SYNC();
   // stage (mj_step1) at the state of the last mj_step1 (pre-teleport), then integrate the current state
   load_state(M, S, w, arena, true);
@@ -3203,7 +3228,9 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
         mx = fabs(f2) > mx ? fabs(f2) : mx;
         if ((double)mx > M.force_thr) hit = true;
       }
-      if (LANE == 0) sc_[3] = __ballot(hit) != 0ull ? 1.0 : 0.0;
+      // the ballot runs on the whole wave (inside `if (LANE == 0)` it would only see lane 0's contacts)
+      const bool any_hit = __ballot(hit) != 0ull;
+      if (LANE == 0) sc_[3] = any_hit ? 1.0 : 0.0;
     }
     // gripper sites at the final state (the last mj_step1's site_xpos)
     arm_hinge_sincos(M, w);
@@ -3213,10 +3240,12 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, false>(M, w, e / 10, e % 10);
     SYNC();
     // stage state for the next env-step = state before the TaskManager's teleports
-    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
-    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
+    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.qd()[i];
+    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.vd()[i];
     if (LANE == 0) task_tail(M, w, ti, td, rng, ctr, act);
     FULL_SYNC();
+    SYNC();
+    refresh_copies(M, w);  // the TaskManager's teleports wrote the master state
     SYNC();
     const int term = sc_[1] != 0.0;
     if (LANE == 0) {
@@ -3255,20 +3284,21 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     FULL_SYNC();
     if (io.terminal_obs) write_obs(M, w, ti, io.terminal_obs + (size_t)arena * dm.obs_dim);
     SYNC();
-    for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = T(0);
+    for (int i = LANE; i < dm.nq; i += WAVE) w.qd()[i] = 0.0;
     for (int i = LANE; i < dm.nv; i += WAVE) {
-      w.v()[i] = T(0);
+      w.vd()[i] = 0.0;
       w.a()[i] = T(0);
     }
     SYNC();
     if (LANE == 0) {
-      task_reset<T, DIM>(M, w.q(), w.v(), ti, td, w.ctrl());
+      task_reset<T, DIM>(M, w.qd(), w.vd(), ti, td, w.ctrl());
       td[3 + 2 * A] = 0.0;
       ti[2 * K + I_EPLEN] = 0;
     }
     SYNC();
-    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.q()[i];
-    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.v()[i];
+    refresh_copies(M, w);
+    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.qd()[i];
+    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.vd()[i];
     reset_pass = true;
   }
   store_state(M, S, w, arena);
@@ -3305,10 +3335,10 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
   const DIM dm(M.dm);
   Ws<T, DIM> w{lds_base(smem), &L};
   int64_t* ctr = S.counters + FM_NCTR * (size_t)arena;
-  const T* ph = S.phys + (size_t)arena * dm.phys_stride;
+  const double* ph = S.phys + (size_t)arena * dm.phys_stride;
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < dm.nu; u += WAVE) w.ctrl()[u] = dsrc[u];
-  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
+  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = (T)ph[2 * dm.nq + 2 * dm.nv + i];
   init_arena(M, w, arena);
   SYNC();
   load_state(M, S, w, arena, true);
