@@ -170,6 +170,9 @@ static int create_typed(fm_handle* h) {
   std::vector<double> arm_base(12 * s.A), body(32 * ARM_NB, 0.0), dof(4 * ARM_ND, 0.0), ctrl(2 * s.nu);
   for (int i = 0; i < s.A; i++)
     for (int k = 0; k < 12; k++) arm_base[12 * i + k] = s.arm_base[i][k];
+  // world -> kernel frame (zshift, fm_dev.hpp): every absolute position the kernel reads
+  const double zs = zshift<T>();
+  for (int i = 0; i < s.A; i++) arm_base[12 * i + 2] -= zs;
   for (int b = 0; b < ARM_NB; b++) {
     double* o = &body[32 * b];
     for (int k = 0; k < 12; k++) o[k] = s.body_local[b][k];
@@ -201,6 +204,7 @@ static int create_typed(fm_handle* h) {
   for (int g = 0; g < ngc; g++) {
     const GeomRec& r = s.geoms[g];
     for (int k = 0; k < 3; k++) geom[16 * g + k] = r.pos[k];
+    if (r.kbody == 0) geom[16 * g + 2] -= zs;  // static geoms: world positions
     for (int k = 0; k < 9; k++) geom[16 * g + 3 + k] = r.R[k];
     for (int k = 0; k < 3; k++) geom[16 * g + 12 + k] = r.size[k];
     geom[16 * g + 15] = r.rbound;
@@ -246,6 +250,7 @@ static int create_typed(fm_handle* h) {
         cbs[8 * b + 4 + k] = c.e[k];
       }
       cbs[8 * b + 3] = c.r;
+      if (c.flags & CB_STATIC) cbs[8 * b + 2] -= zs;
     }
     if ((r = upload_raw<int>(h, &h->ginfo, gin))) return r;
     if ((r = upload_raw<int>(h, &h->cbi, cbi))) return r;

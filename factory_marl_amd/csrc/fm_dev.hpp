@@ -187,6 +187,15 @@ struct Lay {
   int total;
 };
 
+// fp32 builds place the world origin of the float copies at z = 1 m (the table / belt height): contact
+// geometry then works with coordinates of 0..0.2 m instead of ~1.1 m, i.e. 8x finer float spacing in the
+// contact distances the soft constraints amplify.  The float64 master state, the task layer, observations
+// and the buckets stay in the reference's world frame.  fp64 builds use the world frame throughout.
+template <typename T>
+__host__ __device__ constexpr double zshift() {
+  return sizeof(T) == 4 ? 1.0 : 0.0;
+}
+
 // per-contact real record; the Jacobian block first, so its three rows of CJ (even) start 8-byte aligned
 // (records are CR_N = 84 reals, a multiple of 16 bytes) and read as 64-bit LDS loads
 enum { CR_J = 0, CR_DIST = CR_J + 3 * CJ, CR_MU, CR_D, CR_KD, CR_BD, CR_POS, CR_FR = CR_POS + 3, CR_VEL = CR_FR + 9,

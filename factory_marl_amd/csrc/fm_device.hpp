@@ -591,15 +591,15 @@ struct Emit {
 
 template <typename T, typename E>
 __device__ __forceinline__ void np_plane_sphere(const T* c, T r, E& emit) {
-  // floor plane: origin, normal +z (scene.xml:21)
-  T dist = c[2] - r;
+  // floor plane: world origin (z = -zshift in the kernel frame), normal +z (scene.xml:21)
+  T dist = c[2] + T(zshift<T>()) - r;
   if (dist > T(0)) return;
   emit(dist, c[0], c[1], c[2] - (r + dist / T(2)), T(0), T(0), T(1));
 }
 
 template <typename T, typename E>
 __device__ __forceinline__ void np_plane_box(const T* p, const T* R, const T* h, E& emit) {
-  T dist = p[2];
+  T dist = p[2] + T(zshift<T>());
   int cnt = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -988,7 +988,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     } else if (kb == 1) {
       o[0] = 0;
       o[1] = q[0];
-      o[2] = T(1.05);
+      o[2] = T(1.05 - zshift<T>());
     } else if (kb < 2 + K) {
       const T* c = q + 1 + 7 * (kb - 2);
       o[0] = c[0];
@@ -1017,7 +1017,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     } else if (kb == 1) {
       o[0] = T(0);
       o[1] = q[0];
-      o[2] = T(1.05);
+      o[2] = T(1.05 - zshift<T>());
     } else if (kb < 2 + K) {
       const T* c = q + 1 + 7 * (kb - 2);
       o[0] = c[0];
@@ -1051,7 +1051,8 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     d2 = d2 > T(0) ? d2 : T(0);
     const T rr = X[3] + Y[3];
     const bool hs = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
-    const bool hp1 = Y[2] - Y[6] - Y[3] <= T(0), hp2 = X[2] - X[6] - X[3] <= T(0);
+    const T zf = T(-zshift<T>());  // the floor's height in the kernel frame
+    const bool hp1 = Y[2] - Y[6] - Y[3] <= zf, hp2 = X[2] - X[6] - X[3] <= zf;
     const bool hit = pidx < dm.ncbp && ((f1 & CB_PLANE) ? hp1 : ((f2 & CB_PLANE) ? hp2 : hs));
     const int ncomb = hit ? n1 * n2 : 0;
     const uint64_t bal = __ballot(hit);
@@ -1935,6 +1936,9 @@ __device__ __forceinline__ double readlane(double x, int l) {
 }
 
 __device__ __forceinline__ float lane_bcast(float x, int l) { return readlane(x, l); }
+// fp64 broadcast: ds_bpermute (__shfl) by default; FM_F64_READLANE=1 uses the split 64-bit v_readlane.
+// Both pass the fp64 parity tests since SYNC() became a real wave barrier + fences (round 2): the earlier
+// "miscompile" of the readlane form was the compiler-only barrier letting LDS traffic move across it.
 #ifndef FM_F64_READLANE
 #define FM_F64_READLANE 0
 #endif
@@ -2765,7 +2769,7 @@ __device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T
     qq[5] = qu[0] * qr[2] - qu[1] * qr[3] + qu[2] * qr[0] + qu[3] * qr[1];
     qq[6] = qu[0] * qr[3] + qu[1] * qr[2] - qu[2] * qr[1] + qu[3] * qr[0];
     if constexpr (sizeof(T) != 8)
-      for (int c = 0; c < 7; c++) q[1 + 7 * k + c] = (T)qq[c];
+      for (int c = 0; c < 7; c++) q[1 + 7 * k + c] = (T)(c == 2 ? qq[c] - zshift<T>() : qq[c]);
   }
   int qa0 = 1 + 7 * K;
   for (int i = LANE; i < 9 * dm.A; i += WAVE) {
@@ -2944,7 +2948,7 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
       int bi = -1;
       for (int c = 0; c < ts[I_NIN]; c++) {
         const double* qq = w.qd() + 1 + 7 * ti[c];
-        double dx = qq[0] - (double)gp[0], dy = qq[1] - (double)gp[1], dz = qq[2] - (double)gp[2];
+        double dx = qq[0] - (double)gp[0], dy = qq[1] - (double)gp[1], dz = qq[2] - ((double)gp[2] + zshift<T>());
         double dd = sqrt(dx * dx + dy * dy + dz * dz);
         if (bi < 0 || dd < best) {
           best = dd;
@@ -3029,7 +3033,10 @@ template <typename T, typename DIM>
 __device__ __forceinline__ void refresh_copies(const Model<T>& M, const Ws<T, DIM>& w) {
   if constexpr (sizeof(T) != 8) {
     const DIM dm(M.dm);
-    for (int i = LANE; i < dm.nq; i += WAVE) w.q()[i] = (T)w.qd()[i];
+    for (int i = LANE; i < dm.nq; i += WAVE) {
+      const bool cz = i >= 1 && i < 1 + 7 * dm.K && (i - 1) % 7 == 2;  // cube z in the kernel frame
+      w.q()[i] = (T)(cz ? w.qd()[i] - zshift<T>() : w.qd()[i]);
+    }
     for (int i = LANE; i < dm.nv; i += WAVE) w.v()[i] = (T)w.vd()[i];
   }
 }
@@ -3364,11 +3371,13 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
     o[3 * nv + i] = (double)w.fc()[i];
   }
   o += 4 * nv;
-  for (int i = LANE; i < 3 * A; i += WAVE) o[i] = (double)w.site()[i];
+  // positions back in the world frame (zshift)
+  const double zs = zshift<T>();
+  for (int i = LANE; i < 3 * A; i += WAVE) o[i] = (double)w.site()[i] + (i % 3 == 2 ? zs : 0.0);
   o += 3 * A;
   for (int i = LANE; i < 30 * A; i += WAVE) {
-    o[i] = (double)w.bpos()[i];
-    o[30 * A + i] = (double)w.bcom()[i];
+    o[i] = (double)w.bpos()[i] + (i % 3 == 2 ? zs : 0.0);
+    o[30 * A + i] = (double)w.bcom()[i] + (i % 3 == 2 ? zs : 0.0);
   }
   o += 60 * A;
   for (int i = LANE; i < 27 * A; i += WAVE) o[i] = (double)w.dax()[i];
@@ -3381,7 +3390,7 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
       r[0] = M.geom_i[4 * (ci[0] & 4095)];
       r[1] = M.geom_i[4 * ((ci[0] >> 12) & 4095)];
       r[2] = cr[CR_DIST];
-      for (int k = 0; k < 3; k++) r[3 + k] = cr[CR_POS + k];
+      for (int k = 0; k < 3; k++) r[3 + k] = (double)cr[CR_POS + k] + (k == 2 ? zs : 0.0);
       for (int k = 0; k < 9; k++) r[6 + k] = cr[CR_FR + k];
       r[15] = cr[CR_MU];
       r[16] = cr[CR_D];

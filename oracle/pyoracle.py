@@ -83,6 +83,7 @@ def lib():
             "or_d_efc_aref": (DP, [P]), "or_d_efc_J": (DP, [P]), "or_d_stage_fwd": (DP, [P, P, I]),
             "or_env_import": (None, [P, P, P, P]),
             "or_batch_bench": (D, [I, I, I, I, I, U64, P]),
+            "or_set_accel_noise": (None, [D, U64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -105,6 +105,21 @@ static void quat_integrate(double* q, const double* w, double dt) {
   or_quat_mul(q, q, qr);
 }
 
+/* sensitivity probe (tools/fp32_floor.py, not part of the restated algorithm): each substep's acceleration
+ * is multiplied by 1 + amp*U(-1,1), amp = 2^-24 modelling a single fp32 rounding per component; 0 = off */
+static double g_acc_noise = 0.0;
+static uint64_t g_noise_state = 0x9E3779B97F4A7C15ull;
+void or_set_accel_noise(double amp, uint64_t seed) {
+  g_acc_noise = amp;
+  g_noise_state = seed * 0x9E3779B97F4A7C15ull + 1;
+}
+static double noise_u(void) { /* xorshift64*, uniform in [-1, 1) */
+  g_noise_state ^= g_noise_state >> 12;
+  g_noise_state ^= g_noise_state << 25;
+  g_noise_state ^= g_noise_state >> 27;
+  return (double)((g_noise_state * 0x2545F4914F6CDD1Dull) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
 void or_implicit(const or_model* m, or_data* d) {
   int nv = m->nv;
   double dt = m->timestep;
@@ -127,6 +142,8 @@ void or_implicit(const or_model* m, or_data* d) {
   double* qa = d->scratch + 5 * nv * nv;
   for (int i = 0; i < nv; i++) qa[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
   or_chol_solve(MhB, nv, qa);
+  if (g_acc_noise > 0)
+    for (int i = 0; i < nv; i++) qa[i] *= 1.0 + g_acc_noise * noise_u();
   for (int i = 0; i < nv; i++) d->qvel[i] += dt * qa[i];
   for (int j = 0; j < m->njnt; j++) {
     int qa_ = m->jnt_qposadr[j], da = m->jnt_dofadr[j];

@@ -1,13 +1,16 @@
 """Build-recipe guards for factory_marl_amd/csrc/Makefile (CPU only).
 
-The fp32 scene kernels are built with -fno-slp-vectorize (faster); the same flag on the fully unrolled fp64
-fixed-scene kernel miscompiles silently (the fp64 teacher-forced parity tests fail by orders of magnitude), so the
-fp64 objects must keep the default flags.  These checks catch a recipe edit that would reintroduce that.
+The scene kernels are built as one object per (scene, precision) so each precision gets its own flags: the
+fp32 objects add -fno-slp-vectorize (+4.6 % env-steps/s).  Round 1 kept that flag off the fp64
+objects after their parity failed with it; round 2 traced the failure to the compiler-only SYNC() (no wave
+barrier, no fences) and, with SYNC() a real wave barrier, both flag sets pass the fp64 parity sweep
+identically (gpurun_out/r02a, profiles/r02_parity.md).  These checks keep the per-precision split.
 """
 import pathlib
 import re
 
 MAKEFILE = pathlib.Path(__file__).resolve().parents[1] / "factory_marl_amd" / "csrc" / "Makefile"
+DEVICE = pathlib.Path(__file__).resolve().parents[1] / "factory_marl_amd" / "csrc" / "fm_device.hpp"
 
 
 def _rules():
@@ -24,10 +27,20 @@ def test_fixed_objects_split_by_precision():
     assert "-DFM_PREC=32" in rules["32"] and "-DFM_PREC=64" in rules["64"]
 
 
-def test_slp_flag_only_on_fp32_objects():
+def test_slp_flag_on_fp32_objects():
     text, rules = _rules()
     hipflags = re.search(r"^HIPFLAGS \?=(.*(?:\\\n.*)*)", text, re.M).group(1)
     assert "-fno-slp-vectorize" not in hipflags
     assert "$(F32FLAGS)" in rules["32"]
-    assert "$(F32FLAGS)" not in rules["64"] and "slp" not in rules["64"]
-    assert re.search(r"^F64FLAGS \?=\s*$", text, re.M), "fp64 objects must build with the default flags"
+    assert "$(F64FLAGS)" in rules["64"]
+
+
+def test_sync_is_a_wave_barrier_with_fences():
+    """the lanes of an arena hand data to each other through LDS: SYNC() must be a wave barrier plus
+    wavefront-scope release/acquire fences, not a compiler-only memory clobber"""
+    src = DEVICE.read_text()
+    m = re.search(r"#define SYNC\(\)(.*?)while \(0\)", src, re.S)
+    assert m, "SYNC() macro not found"
+    body = m.group(1)
+    assert "__builtin_amdgcn_wave_barrier" in body
+    assert "__ATOMIC_RELEASE" in body and "__ATOMIC_ACQUIRE" in body and '"wavefront"' in body

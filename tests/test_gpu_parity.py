@@ -70,20 +70,32 @@ def test_teacher_forced_fp64(trajectory):
     assert r["counters"][:, 0].sum() == 0  # no contacts dropped for capacity
 
 
+@pytest.fixture(scope="module")
+def long_trajectory(oracle):
+    """300 env-steps from reset: every cube of the (2, 4) scene spawned, landed, scored or dropped, a force
+    termination and its auto-reset (seed 21)"""
+    return _rollout(oracle, A, K, 300, seed_actions=21)
+
+
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-def test_teacher_forced_fp32(trajectory):
-    r = _compare(trajectory, "fp32", 1e-4)
+@pytest.mark.parametrize("which", ["short", "long"])
+def test_teacher_forced_fp32(trajectory, long_trajectory, which):
+    r = _compare(trajectory if which == "short" else long_trajectory, "fp32", 1e-4)
     e = r["errs"]
     frac = float(np.mean(e <= 1e-4))
     print(f"fp32 teacher-forced (SURVEY tolerance 1e-4 rel): {frac:.1%} of {len(e)} steps within; "
           f"median {np.median(e):.2e}, worst {e.max():.2e}; integer/flag divergences "
-          f"{len(r['int_bad'])}/{len(r['flag_bad'])}; obs worst {r['obs_err'].max():.2e}")
+          f"{len(r['int_bad'])}/{len(r['flag_bad'])}; obs worst {r['obs_err'].max():.2e}; "
+          f"missing steps {list(r['err_steps'][e > 1e-4])}")
     assert not r["flag_bad"], r["flag_bad"]
     assert len(r["int_bad"]) == 0, r["int_bad"]
-    # fp32 holds the SURVEY gate on ~90 % of teacher-forced env-steps; the rest are discrete contact
-    # events (pyramid-edge activation, face/edge box-box choice) that flip under fp32 rounding within the
-    # 100 substeps.  The fp64 build holds 1e-7 on every step (test above).
-    assert frac >= 0.85
+    # fp32 physics over a float64 master state in a z-shifted frame (DESIGN.md §3): measured 95.8 % (96 steps)
+    # and 94.6-95.2 % (300 steps, median 1.1e-5 - 2.2e-5).  The misses are the landing impacts of freshly
+    # spawned cubes (env-steps 4-5, 52-53, 97 after each reset, in every trajectory) and a few contact
+    # transitions; tools/fp32_floor.py --accel-noise shows the float64 oracle itself misses those steps under a
+    # 1e-4 relative per-substep acceleration perturbation
+    assert frac >= 0.94
+    assert np.median(e) <= 3e-5
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
@@ -162,16 +174,31 @@ def test_teacher_forced_fp64_other_configs(oracle, A_, K_, env_class, reward):
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-def test_fp32_other_scene_within_survey_gate(oracle):
-    """fp32 (2, 8) compile-time scene: integer state / flags exact, SURVEY gate on most env-steps"""
-    traj = _rollout(oracle, 2, 8, 48, seed_actions=5)
-    r = _compare(traj, "fp32", 1e-4, 2, 8)
-    frac = float(np.mean(r["errs"] <= 1e-4))
-    print(f"fp32 (2,8): {frac:.1%} of {len(r['errs'])} steps within 1e-4; median {np.median(r['errs']):.2e}")
-    assert not r["flag_bad"] and len(r["int_bad"]) == 0
-    # measured 79 % on this 48-step trajectory (the (2, 4) scene: 90 %): more cubes, more contact events that
-    # flip under fp32 rounding inside the 100 substeps; the fp64 build holds 1e-7 on every step of it
-    assert frac >= 0.75
+@pytest.mark.parametrize("A_,K_,T,seed", [(2, 4, 300, 21), (2, 8, 300, 5), (2, 10, 250, 9)])
+def test_teacher_forced_long_fp64(oracle, A_, K_, T, seed):
+    """>= 250 env-steps from reset (every cube spawned, cube-cube contacts, force terminations with their
+    auto-resets): fp64 within 1e-7 per env-step, integer state / RNG / scores / flags bit-exact"""
+    traj = _rollout(oracle, A_, K_, T, seed_actions=seed)
+    r = _compare(traj, "fp64", 1e-7, A_, K_)
+    print(f"fp64 ({A_},{K_}) x {T}: worst {r['errs'].max():.3e}, terminations {r['terms']}, "
+          f"max cubes {r['max_cubes']}")
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    assert r["errs"].max() <= 1e-7
+    assert r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
+    assert r["counters"][:, 0].sum() == 0
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_fp32_other_scenes_within_survey_gate(oracle):
+    """fp32 (2, 8) and (2, 10) compile-time scenes over long trajectories: integer state / flags exact, the
+    SURVEY gate on >= 94 % of env-steps (measured 95.0 % and 95.2 %)"""
+    for A_, K_, T, seed in [(2, 8, 300, 5), (2, 10, 250, 9)]:
+        traj = _rollout(oracle, A_, K_, T, seed_actions=seed)
+        r = _compare(traj, "fp32", 1e-4, A_, K_)
+        frac = float(np.mean(r["errs"] <= 1e-4))
+        print(f"fp32 ({A_},{K_}): {frac:.1%} of {len(r['errs'])} steps within 1e-4; median {np.median(r['errs']):.2e}")
+        assert not r["flag_bad"] and len(r["int_bad"]) == 0
+        assert frac >= 0.94
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")

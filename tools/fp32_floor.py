@@ -8,7 +8,12 @@ that rounded state and compares with the unrounded step, with the SURVEY §8(d) 
 ANY fp32-state implementation of the algorithm: the miss is inherent (input rounding amplified by the
 step's contact events), not the kernel's arithmetic.
 
-usage: python tools/fp32_floor.py [A K T seed_actions] [--json out.json]
+Second probe (--accel-noise AMP): the float64 oracle steps from the exact state, but every substep's
+acceleration is multiplied by 1 + AMP*U(-1,1) (AMP = 2^-24 models ONE fp32 rounding per component per
+substep, the least any fp32 physics incurs).  Steps that miss the gate under that perturbation are
+sensitive beyond fp32 resolution: their miss is inherent to fp32 arithmetic, not to a kernel.
+
+usage: python tools/fp32_floor.py [A K T seed_actions] [--accel-noise AMP] [--json out.json]
 """
 import json
 import os
@@ -27,7 +32,7 @@ def rel_err(A, K, got, ref):
     return float(max(qd.max(), vd.max()))
 
 
-def floor_study(A, K, T, seed_actions=7, amp=1.0, rng_perturb=None):
+def floor_study(A, K, T, seed_actions=7, amp=1.0, rng_perturb=None, accel_noise=0.0):
     """returns per-step (rel err of the rounded-start step vs the exact step, terminated, flag flips)"""
     nq, nv = 1 + 7 * K + 9 * A, 1 + 6 * K + 9 * A
     nphys = 2 * nq + 3 * nv
@@ -41,13 +46,18 @@ def floor_study(A, K, T, seed_actions=7, amp=1.0, rng_perturb=None):
         d, i, r = e.export_state()
         a = rng.uniform(-2, 2, 8 * A).astype(np.float32)
         dp = d.copy()
-        if rng_perturb is None:
+        if accel_noise > 0:
+            pass  # exact start, perturbed substeps
+        elif rng_perturb is None:
             dp[:nphys] = dp[:nphys].astype(np.float32).astype(np.float64)
         else:  # random relative perturbation of amplitude amp * 2^-24 (float32 half-ulp scale)
             dp[:nphys] *= 1 + amp * 2.0 ** -24 * rng_perturb.uniform(-1, 1, nphys)
         p.import_state(dp, i, r)
         _, _, term, _, info = e.step(a)
+        if accel_noise > 0:
+            po.lib().or_set_accel_noise(accel_noise, t + 1)
         _, _, pterm, _, pinfo = p.step(a)
+        po.lib().or_set_accel_noise(0.0, 0)
         d2, i2, _ = e.export_state()
         p2, pi2, _ = p.export_state()
         flip = (term != pterm) or not np.array_equal(i2, pi2)
@@ -66,11 +76,20 @@ def summarize(rows, gate=1e-4):
 
 
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
+    noise = 0.0
+    if "--accel-noise" in argv:
+        noise = float(argv[argv.index("--accel-noise") + 1])
+        del argv[argv.index("--accel-noise"):argv.index("--accel-noise") + 2]
+    jpath = None
+    if "--json" in argv:
+        jpath = argv[argv.index("--json") + 1]
+        del argv[argv.index("--json"):argv.index("--json") + 2]
+    args = [a for a in argv if not a.startswith("--")]
     A, K, T, sa = (int(x) for x in (args + ["2", "4", "96", "7"][len(args):]))
     po.build()
-    rows = floor_study(A, K, T, sa)
+    rows = floor_study(A, K, T, sa, accel_noise=noise)
     s = summarize(rows)
-    print(json.dumps(dict(A=A, K=K, T=T, seed_actions=sa, **s)))
-    if "--json" in sys.argv:
-        json.dump(dict(summary=s, rows=rows), open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+    print(json.dumps(dict(A=A, K=K, T=T, seed_actions=sa, accel_noise=noise, **s)))
+    if jpath:
+        json.dump(dict(summary=s, rows=rows), open(jpath, "w"), indent=1)
