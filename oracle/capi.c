@@ -117,7 +117,9 @@ void or_task_free(or_task* t) { free(t); }
  *      fm_get_state / fm_set_state): doubles [qpos nq | qvel nv | qpos_stage nq | qvel_stage nv |
  *      qacc_warmstart nv | ctrl_target nu | spawn_freq | speed | play_time | last_grip A |
  *      last_bucket A | ep_return], int32 [in K | out K | n_in n_out step since fail hidden s0 s1 ls0 ls1 eplen],
- *      uint64 [state_hi state_lo inc_hi inc_lo] */
+ *      uint64 [state_hi state_lo inc_hi inc_lo]
+ *      IK block (every env class): doubles A x [last_ctrl 8 | move_start 3 | ik_actions 8 | pause_last 8]
+ *      after ep_return, int32 A x [state counter target ignore[A]] after eplen */
 void or_env_export(const or_env* e, double* dbl, int32_t* ints, uint64_t* rng) {
   const or_model* m = e->m;
   const or_data* d = e->d;
@@ -136,6 +138,12 @@ void or_env_export(const or_env* e, double* dbl, int32_t* ints, uint64_t* rng) {
   for (int i = 0; i < A; i++) *p++ = t->last_grip_dist[i];
   for (int i = 0; i < A; i++) *p++ = t->last_bucket_dist[i];
   *p++ = e->ep_return;
+  for (int i = 0; i < A; i++) {
+    memcpy(p, e->ik[i].last_ctrl, 8 * sizeof(double)); p += 8;
+    memcpy(p, e->ik[i].move_start, 3 * sizeof(double)); p += 3;
+    memcpy(p, e->ik_actions[i], 8 * sizeof(double)); p += 8;
+    memcpy(p, e->pause_last[i], 8 * sizeof(double)); p += 8;
+  }
   int32_t* q = ints;
   for (int k = 0; k < K; k++) q[k] = k < t->n_in ? t->in_scene[k] : -1;
   for (int k = 0; k < K; k++) q[K + k] = k < t->n_out ? t->out_scene[k] : -1;
@@ -143,6 +151,11 @@ void or_env_export(const or_env* e, double* dbl, int32_t* ints, uint64_t* rng) {
   q[0] = t->n_in; q[1] = t->n_out; q[2] = t->step_counter; q[3] = t->steps_since_spawn;
   q[4] = t->failure_counter; q[5] = t->hidden_counter; q[6] = t->scores[0]; q[7] = t->scores[1];
   q[8] = t->last_score[0]; q[9] = t->last_score[1]; q[10] = e->ep_len;
+  q += 11;
+  for (int i = 0; i < A; i++) {
+    *q++ = e->ik[i].state; *q++ = e->ik[i].counter; *q++ = e->ik[i].target;
+    for (int o = 0; o < A; o++) *q++ = e->ik[i].ignore[o];
+  }
   rng[0] = t->rng.state_hi; rng[1] = t->rng.state_lo; rng[2] = t->rng.inc_hi; rng[3] = t->rng.inc_lo;
 }
 
@@ -165,10 +178,25 @@ void or_env_import(or_env* e, const double* dbl, const int32_t* ints, const uint
   for (int i = 0; i < A; i++) t->last_grip_dist[i] = *p++;
   for (int i = 0; i < A; i++) t->last_bucket_dist[i] = *p++;
   e->ep_return = *p++;
+  for (int i = 0; i < A; i++) {
+    memcpy(e->ik[i].last_ctrl, p, 8 * sizeof(double)); p += 8;
+    memcpy(e->ik[i].move_start, p, 3 * sizeof(double)); p += 3;
+    memcpy(e->ik_actions[i], p, 8 * sizeof(double)); p += 8;
+    memcpy(e->pause_last[i], p, 8 * sizeof(double)); p += 8;
+  }
   const int32_t* q = ints + 2 * K;
   t->n_in = q[0]; t->n_out = q[1]; t->step_counter = q[2]; t->steps_since_spawn = q[3];
   t->failure_counter = q[4]; t->hidden_counter = q[5]; t->scores[0] = q[6]; t->scores[1] = q[7];
   t->last_score[0] = q[8]; t->last_score[1] = q[9]; e->ep_len = q[10];
+  {
+    const int32_t* r = q + 11;
+    for (int i = 0; i < A; i++) {
+      e->ik[i].state = *r++; e->ik[i].counter = *r++; e->ik[i].target = *r++;
+      for (int o = 0; o < A; o++) e->ik[i].ignore[o] = *r++;
+    }
+    for (int i = 0; i < A; i++)
+      for (int o = 0; o < A; o++) t->ik_ignore[i][o] = e->ik[i].ignore[o];
+  }
   for (int k = 0; k < K; k++) t->in_scene[k] = ints[k];
   for (int k = 0; k < K; k++) t->out_scene[k] = ints[K + k];
   t->rng.state_hi = rng[0]; t->rng.state_lo = rng[1]; t->rng.inc_hi = rng[2]; t->rng.inc_lo = rng[3];
@@ -215,3 +243,94 @@ double or_batch_bench(int A, int K, int n, int steps, int threads, uint64_t seed
   if (env_steps_out) *env_steps_out = total;
   return dt;
 }
+
+/* ---- IK policy pieces on flat arrays (tests/test_oracle_golden.py replays the reference's FSM) ----
+ * arm_i = [state, counter, target, ignore[16]], arm_d = [last_ctrl 8, move_start 3] */
+static void arm_from_flat(or_ik_arm* p, const int* ai, const double* ad) {
+  p->state = ai[0];
+  p->counter = ai[1];
+  p->target = ai[2];
+  for (int o = 0; o < OR_IK_MAXA; o++) p->ignore[o] = ai[3 + o];
+  memcpy(p->last_ctrl, ad, 8 * sizeof(double));
+  memcpy(p->move_start, ad + 8, 3 * sizeof(double));
+}
+static void arm_to_flat(const or_ik_arm* p, int* ai, double* ad) {
+  ai[0] = p->state;
+  ai[1] = p->counter;
+  ai[2] = p->target;
+  for (int o = 0; o < OR_IK_MAXA; o++) ai[3 + o] = p->ignore[o];
+  memcpy(ad, p->last_ctrl, 8 * sizeof(double));
+  memcpy(ad + 8, p->move_start, 3 * sizeof(double));
+}
+void or_ik_arm_init_flat(int* ai, double* ad) {
+  or_ik_arm p;
+  or_ik_arm_init(&p);
+  arm_to_flat(&p, ai, ad);
+}
+void or_ik_arm_reset_flat(int* ai, double* ad) {
+  or_ik_arm p;
+  arm_from_flat(&p, ai, ad);
+  or_ik_arm_reset(&p);
+  arm_to_flat(&p, ai, ad);
+}
+int or_ik_plan_flat(int A, int n_in, const int* in_scene, const double* cube_qpos, const double* cube_qvel,
+                    const double* grip, const double* base, const double* bucket, const double* arm_q, int* ai,
+                    double* ad, double* tpos, double* tquat, int* close) {
+  or_ik_arm p;
+  arm_from_flat(&p, ai, ad);
+  or_ik_in in = {A, n_in, in_scene, cube_qpos, cube_qvel, grip, base, bucket, arm_q};
+  int r = or_ik_plan(&in, &p, tpos, tquat, close);
+  arm_to_flat(&p, ai, ad);
+  return r;
+}
+void or_ik_finish_flat(int* ai, double* ad, int success, const double* q7, int close, double* ctrl) {
+  or_ik_arm p;
+  arm_from_flat(&p, ai, ad);
+  or_ik_finish(&p, success, q7, close, ctrl);
+  arm_to_flat(&p, ai, ad);
+}
+int or_env_act_dim(const or_env* e) { return e->act_dim; }
+int or_env_ik_steps(const or_env* e) { return e->ik_steps; }
+void or_env_ik_arm(const or_env* e, int i, int* ai, double* ad) { arm_to_flat(&e->ik[i], ai, ad); }
+
+/* golden replay of FactoryManipulationEnv._compose_control with the reference's (fake) IK results in call
+ * order; the IK arguments of each call are written to args (tpos 3 | tquat 4 per call) */
+typedef struct {
+  const int* success;
+  const double* q7;
+  int n, calls;
+  double* args;
+} rec_solver;
+static int rec_solve(void* ctx, int arm, const double* tp, const double* tq, double* q7) {
+  rec_solver* r = ctx;
+  (void)arm;
+  if (r->calls >= r->n) return 0;
+  memcpy(r->args + 7 * r->calls, tp, 3 * sizeof(double));
+  memcpy(r->args + 7 * r->calls + 3, tq, 4 * sizeof(double));
+  memcpy(q7, r->q7 + 7 * r->calls, 7 * sizeof(double));
+  return r->success[r->calls++];
+}
+int or_ik_compose_replay(const or_model* m, int* arm_i /* A x 19 */, double* arm_d /* A x 11 */, const double* qpos,
+                         const double* qvel, const double* grip, const double* base, const int* in_scene, int n_in,
+                         const int* rec_success, const double* rec_q7, int n_rec, double* args_out,
+                         double* arm_ctrl) {
+  or_ik_arm ik[OR_IK_MAXA];
+  for (int i = 0; i < m->A; i++) arm_from_flat(&ik[i], arm_i + 19 * i, arm_d + 11 * i);
+  rec_solver r = {rec_success, rec_q7, n_rec, 0, args_out};
+  or_ik_compose(m, ik, qpos, qvel, grip, base, in_scene, n_in, rec_solve, &r, arm_ctrl);
+  for (int i = 0; i < m->A; i++) arm_to_flat(&ik[i], arm_i + 19 * i, arm_d + 11 * i);
+  return r.calls;
+}
+void or_t_set_ignore(or_task* t, int arm, const int* values, int n) {
+  for (int o = 0; o < 16; o++) t->ik_ignore[arm][o] = o < n ? values[o] : -1;
+}
+void or_t_set_act_dim(or_task* t, int act_dim) { t->act_dim = act_dim; }
+void or_t_set_in_scene(or_task* t, const int* list, int n) {
+  t->n_in = n;
+  for (int i = 0; i < n; i++) t->in_scene[i] = list[i];
+}
+void or_t_set_scores(or_task* t, int s0, int s1) {
+  t->scores[0] = s0;
+  t->scores[1] = s1;
+}
+void or_t_reset_reward_state(or_task* t) { t->last_score[0] = t->last_score[1] = 0; } /* reset(): last_score */

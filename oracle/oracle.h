@@ -149,23 +149,69 @@ typedef struct or_task {
   int last_score[2];
   double w_grip, w_bucket, w_action, base_reward;
   int reward_kind; /* 0: score delta (FactoryManipulationEnv), 1: progress (ProgressRewardEnv) */
+  int ik_ignore[16][16]; /* IKPolicy.ignore_objects of arm i: owner arm -> cube index, -1 = none (reward candidates) */
+  int act_dim;           /* action_space.shape[0] of the env class (progress-reward action norm) */
   /* config (BaseEnv.__init__ kwargs, base_env.py:15-35) */
   double initial_conveyor_speed, conveyor_acceleration, pt_time, force_contact_threshold, spawn_freq_increase;
   int frame_skip;
 } or_task;
 
+/* ---------------- IK base policy (ik.c; ik_policy.py) ---------------- */
+#define OR_IK_MAXA 16
+enum { OR_IK_IDLE = 0, OR_IK_GO_TO_GRASP, OR_IK_GRASP_APPROACH, OR_IK_GRASP_CLOSE, OR_IK_POST_GRASP,
+       OR_IK_GO_TO_RELEASE, OR_IK_RELEASE };
+typedef struct or_ik_arm {
+  int state, counter, target; /* PolicyState, state_counter, target_object (cube index, -1 = None) */
+  int ignore[OR_IK_MAXA];     /* ignore_objects: owner arm -> cube index, -1 = None / never set */
+  double last_ctrl[8], move_start[3];
+} or_ik_arm;
+/* what IKPolicy.act reads from the physics (all world frame, float64) */
+typedef struct or_ik_in {
+  int A, n_in;
+  const int* in_scene;      /* TaskManager._in_scene order */
+  const double* cube_qpos;  /* [K][7] */
+  const double* cube_qvel;  /* [K][6] */
+  const double* grip;       /* site_xpos of between_gripper_plates */
+  const double* base;       /* site_xpos of player_site */
+  const double* bucket;     /* xpos of this arm's bucket (buckets[i % 2]) */
+  const double* arm_q;      /* the 7 hinge qpos */
+} or_ik_in;
+extern const double OR_IK_DEFAULT_POSE[8];
+void or_ik_arm_init(or_ik_arm* p);
+void or_ik_arm_reset(or_ik_arm* p);
+void or_ik_grasp_quat(const double obj_quat_wxyz[4], double out_wxyz[4]);
+int or_ik_plan(const or_ik_in* in, or_ik_arm* p, double tpos[3], double tquat[4], int* close_gripper);
+void or_ik_finish(or_ik_arm* p, int success, const double q7[7], int close_gripper, double ctrl[8]);
+int or_ik_solve(const or_model* m, or_data* scratch, const double* qpos, int arm, const double tpos[3],
+                const double tquat[4], double q7[7], int* steps_out);
+typedef int (*or_ik_solver)(void* ctx, int arm, const double* tpos, const double* tquat, double* q7);
+void or_ik_compose(const or_model* m, or_ik_arm* ik, const double* qpos, const double* qvel, const double* grip /*3A*/,
+                   const double* base /*3A*/, const int* in_scene, int n_in, or_ik_solver solve, void* ctx,
+                   double* arm_ctrl /* 8A */);
+void or_compose_class(const or_model* m, int env_class, const float* action, const double* ik, const int* ik_state,
+                      const double* ik_actions, double* pause_last, double* arm_ctrl);
+
+/* env classes (environments.py), same numbering as the product's FM_ENV_* (include/factorysim.h) */
+enum { OR_ENV_FACTORY = 0, OR_ENV_ALLFULLRL = 1, OR_ENV_SINGLEFULLRL = 2, OR_ENV_SINGLEDELTA = 3,
+       OR_ENV_ALLDELTA = 4, OR_ENV_PAUSE_TOGGLE = 5, OR_ENV_BACKUP_TOGGLE = 6 };
+
 typedef struct or_env {
   or_model* m;
   or_data* d;
   or_task t;
-  int obs_dim, act_dim;
+  int obs_dim, act_dim, env_class;
+  or_ik_arm ik[OR_IK_MAXA];
+  double ik_actions[OR_IK_MAXA][8]; /* IKTogglingEnv.ik_actions (proposals of the last observation) */
+  double pause_last[OR_IK_MAXA][8]; /* PauseIKToggleEnv.last_arm_actions */
+  or_data* ik_d;                    /* scratch physics copy of qpos_from_site_pose (inplace=False) */
+  int ik_steps;                     /* diagnostics: IK iterations summed over the last compose */
   double* stage_qpos; /* state at which the current position/velocity stage was computed (last mj_step1) */
   double* stage_qvel;
   double ep_return;
   int ep_len;
 } or_env;
 
-or_env* or_env_create(int A, int K, uint64_t seed, int reward_kind, const double* reward_w /*4*/);
+or_env* or_env_create(int A, int K, uint64_t seed, int env_class, const double* reward_w /*4*/);
 void or_env_free(or_env* e);
 void or_env_reset(or_env* e, float* obs);
 /* one FactoryManipulationEnv.step(): returns terminated; info_out = [score0, score1, play_time,

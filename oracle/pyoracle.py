@@ -84,6 +84,15 @@ def lib():
             "or_env_import": (None, [P, P, P, P]),
             "or_batch_bench": (D, [I, I, I, I, I, U64, P]),
             "or_set_accel_noise": (None, [D, U64]),
+            "or_ik_arm_init_flat": (None, [P, P]), "or_ik_arm_reset_flat": (None, [P, P]),
+            "or_ik_plan_flat": (I, [I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
+            "or_ik_finish_flat": (None, [P, P, I, P, I, P]),
+            "or_ik_grasp_quat": (None, [P, P]),
+            "or_ik_compose_replay": (I, [P, P, P, P, P, P, P, P, I, P, P, I, P, P]),
+            "or_compose_class": (None, [P, I, P, P, P, P, P, P]),
+            "or_t_set_ignore": (None, [P, I, P, I]), "or_t_set_in_scene": (None, [P, P, I]),
+            "or_t_set_scores": (None, [P, I, I]), "or_t_reset_reward_state": (None, [P]), "or_t_set_act_dim": (None, [P, I]),
+            "or_env_act_dim": (I, [P]), "or_env_ik_steps": (I, [P]), "or_env_ik_arm": (None, [P, I, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -275,21 +284,31 @@ class Data:
         return jp.reshape(3, -1), jr.reshape(3, -1)
 
 
+# env classes of src/environments.py (oracle.h OR_ENV_*, include/factorysim.h FM_ENV_*)
+ENV_CLASSES = {"FactoryManipulationEnv": 0, "AllFullRLProgressRewardEnv": 1, "SingleFullRLProgressRewardEnv": 2,
+               "SingleDeltaProgressRewardEnv": 3, "AllDeltaProgressRewardEnv": 4, "PauseIKToggleEnv": 5,
+               "BackupIKToggleEnv": 6}
+IK_STATES = ["IDLE", "GO_TO_GRASP", "GRASP_APPROACH", "GRASP_CLOSE", "POST_GRASP", "GO_TO_RELEASE", "RELEASE"]
+
+
 class Env:
-    """Oracle restatement of AllFullRLProgressRewardEnv / FactoryManipulationEnv (score reward)."""
+    """Oracle restatement of the env classes of src/environments.py (default AllFullRLProgressRewardEnv)."""
 
     def __init__(self, num_arms=2, max_num_objects=4, seed=42, reward="progress",
-                 weights=(0.2, 0.4, 0.0, 0.4)):
+                 weights=(0.2, 0.4, 0.0, 0.4), env_class=None):
         L = lib()
         w = (C.c_double * 4)(*weights)
-        self.h = L.or_env_create(num_arms, max_num_objects, seed, 1 if reward == "progress" else 0, w)
+        if env_class is None:  # legacy selector: progress -> AllFullRL, score -> FactoryManipulationEnv
+            env_class = "AllFullRLProgressRewardEnv" if reward == "progress" else "FactoryManipulationEnv"
+        self.env_class = env_class
+        self.h = L.or_env_create(num_arms, max_num_objects, seed, ENV_CLASSES[env_class], w)
         if not self.h:
             raise ValueError("bad env config")
         self.model = Model(num_arms, max_num_objects, seed, handle=L.or_env_model(self.h))
         self.data = Data(self.model, handle=L.or_env_data(self.h))
         self.task = L.or_env_task(self.h)
         self.obs_dim = L.or_env_obs_dim(self.h)
-        self.act_dim = 8 * num_arms
+        self.act_dim = L.or_env_act_dim(self.h)
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -302,7 +321,7 @@ class Env:
         return obs
 
     def step(self, action):
-        a = np.ascontiguousarray(action, dtype=np.float32)
+        a = np.ascontiguousarray(action if self.act_dim else np.zeros(1), dtype=np.float32)
         obs = np.zeros(self.obs_dim, np.float32)
         rew = C.c_double(0)
         info = (C.c_double * 7)()
@@ -327,9 +346,20 @@ class Env:
 
     def state_sizes(self):
         m = self.model
-        nd = 2 * m.nq + 3 * m.nv + m.nu + 3 + 2 * m.A + 1
-        ni = 2 * m.K + 11
+        nd = 2 * m.nq + 3 * m.nv + m.nu + 3 + 2 * m.A + 1 + 27 * m.A
+        ni = 2 * m.K + 11 + (3 + m.A) * m.A
         return nd, ni
+
+    def ik_arm(self, i):
+        """IKPolicy state of arm i: dict(state, counter, target, ignore, last_ctrl, move_start)"""
+        ai = np.zeros(19, np.int32)
+        ad = np.zeros(11)
+        lib().or_env_ik_arm(self.h, i, ptr(ai), ptr(ad))
+        return dict(state=int(ai[0]), counter=int(ai[1]), target=int(ai[2]), ignore=list(ai[3:3 + self.model.A]),
+                    last_ctrl=ad[:8].copy(), move_start=ad[8:11].copy())
+
+    def ik_steps(self):
+        return lib().or_env_ik_steps(self.h)
 
     def export_state(self):
         """full arena state in the product's record layout (fm_get_state)"""

@@ -36,6 +36,9 @@ void or_task_init(or_task* t, int A, int K, uint64_t seed) {
   t->frame_skip = (int)((1.0 / 10.0) / 0.001);
   or_pcg64_seed(&t->rng, seed);
   t->conveyor_speed = t->initial_conveyor_speed;
+  for (int i = 0; i < 16; i++)
+    for (int j = 0; j < 16; j++) t->ik_ignore[i][j] = -1;
+  t->act_dim = 8 * A;
 }
 
 static int cube_qadr(const or_model* m, int k) { return m->jnt_qposadr[m->body_jntadr[m->cube_body0 + k]]; }
@@ -243,6 +246,10 @@ double or_task_reward(or_task* t, const or_model* m, const double* qpos, const d
       double best = 0;
       int bi = -1;
       for (int c = 0; c < t->n_in; c++) {
+        /* candidates: in-scene cubes this arm's IK policy does not ignore (environments.py:303-304) */
+        int ign = 0;
+        for (int o = 0; o < m->A; o++) ign |= t->ik_ignore[i][o] == t->in_scene[c];
+        if (ign) continue;
         const double* q = qpos + cube_qadr(m, t->in_scene[c]);
         double dv[3] = {q[0] - gp[0], q[1] - gp[1], q[2] - gp[2]};
         double dd = sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
@@ -250,6 +257,10 @@ double or_task_reward(or_task* t, const or_model* m, const double* qpos, const d
           best = dd;
           bi = c;
         }
+      }
+      if (bi < 0) { /* every candidate ignored: (None, last distance, 0) */
+        closest[i] = -1;
+        continue;
       }
       closest[i] = t->in_scene[bi];
       double change = t->last_grip_dist[i] - best;
@@ -272,7 +283,7 @@ double or_task_reward(or_task* t, const or_model* m, const double* qpos, const d
     /* np.exp(-np.linalg.norm(float32 actions)) stays float32; the sum is float64 (numpy 1.26,
        environment.yml:200, scalar promotion) */
     float ss = 0.0f;
-    for (int i = 0; i < 8 * m->A; i++)
+    for (int i = 0; i < t->act_dim; i++)
       if (i % 8 != 7) ss += action[i] * action[i];
     float an = expf(-sqrtf(ss));
     double progress = t->base_reward + t->w_grip * gc + t->w_bucket * bc + t->w_action * (double)an;
@@ -284,9 +295,12 @@ double or_task_reward(or_task* t, const or_model* m, const double* qpos, const d
 }
 
 /* ------------------------------------------------------------------------------------------------
- * full environment: AllFullRLProgressRewardEnv / FactoryManipulationEnv-style score reward
+ * full environment: the env classes of src/environments.py (OR_ENV_*)
  * ------------------------------------------------------------------------------------------------ */
-or_env* or_env_create(int A, int K, uint64_t seed, int reward_kind, const double* w) {
+static int is_toggle(int c) { return c == OR_ENV_PAUSE_TOGGLE || c == OR_ENV_BACKUP_TOGGLE; }
+
+or_env* or_env_create(int A, int K, uint64_t seed, int env_class, const double* w) {
+  if (env_class < OR_ENV_FACTORY || env_class > OR_ENV_BACKUP_TOGGLE || A > OR_IK_MAXA) return NULL;
   or_env* e = calloc(1, sizeof(or_env));
   e->m = or_model_create(A, K, seed);
   if (!e->m) {
@@ -294,24 +308,184 @@ or_env* or_env_create(int A, int K, uint64_t seed, int reward_kind, const double
     return NULL;
   }
   e->d = or_data_create(e->m);
+  e->ik_d = or_data_create(e->m);
   or_task_init(&e->t, A, K, seed);
-  e->t.reward_kind = reward_kind;
+  e->env_class = env_class;
+  /* FactoryManipulationEnv and the IK-toggling envs keep the score-delta reward (environments.py:129-149,
+   * 538-645); the other classes derive from ProgressRewardEnv (environments.py:251-535) */
+  e->t.reward_kind = (env_class == OR_ENV_FACTORY || is_toggle(env_class)) ? 0 : 1;
   if (w) {
     e->t.w_grip = w[0];
     e->t.w_bucket = w[1];
     e->t.w_action = w[2];
     e->t.base_reward = w[3];
   }
-  e->obs_dim = 24 * A + 13 * K;
-  e->act_dim = 8 * A;
+  e->obs_dim = 24 * A + 13 * K + (is_toggle(env_class) ? 8 * A : 0);
+  switch (env_class) {
+    case OR_ENV_FACTORY: e->act_dim = 0; break;
+    case OR_ENV_SINGLEFULLRL:
+    case OR_ENV_SINGLEDELTA: e->act_dim = 8; break;
+    case OR_ENV_PAUSE_TOGGLE:
+    case OR_ENV_BACKUP_TOGGLE: e->act_dim = A; break;
+    default: e->act_dim = 8 * A;
+  }
+  e->t.act_dim = e->act_dim;
+  for (int i = 0; i < A; i++) {
+    or_ik_arm_init(&e->ik[i]); /* IKPolicy(env, arm_id=i, bucket_idx=i % 2) (environments.py:39) */
+    memset(e->pause_last[i], 0, sizeof e->pause_last[i]); /* np.zeros(dof) (environments.py:592) */
+  }
   e->stage_qpos = calloc(e->m->nq, sizeof(double));
   e->stage_qvel = calloc(e->m->nv, sizeof(double));
   return e;
 }
 
+/* FactoryManipulationEnv._compose_control (environments.py:104-127): each arm's IKPolicy.act() in arm
+ * order, clipped to actuator_ctrlrange[1:9]; then every other arm ignores this arm's target.  The IK solve
+ * is a callback: qpos_from_site_pose in the env (or_ik_solve), recorded results in the golden replay. */
+void or_ik_compose(const or_model* m, or_ik_arm* ik, const double* qpos, const double* qvel, const double* grip,
+                   const double* base, const int* in_scene, int n_in, or_ik_solver solve, void* ctx,
+                   double* arm_ctrl /* 8A */) {
+  const int A = m->A, K = m->K;
+  double cq[64 * 7], cv[64 * 6];
+  for (int k = 0; k < K; k++) {
+    memcpy(cq + 7 * k, qpos + cube_qadr(m, k), 7 * sizeof(double));
+    memcpy(cv + 6 * k, qvel + cube_dadr(m, k), 6 * sizeof(double));
+  }
+  for (int i = 0; i < A; i++) {
+    or_ik_arm* p = &ik[i];
+    const double bucket[3] = {(i % 2) == 0 ? 0.9 : -0.9, 0.7 - (A / 2 - 1), 1.05 - 0.04};
+    or_ik_in in = {A, n_in, in_scene, cq, cv, grip + 3 * i, base + 3 * i, bucket, qpos + 1 + 7 * K + 9 * i};
+    double tp[3], tq[4], ctrl[8];
+    int close = 0;
+    if (or_ik_plan(&in, p, tp, tq, &close)) {
+      double q7[7];
+      int ok = solve(ctx, i, tp, tq, q7);
+      or_ik_finish(p, ok, q7, close, ctrl);
+    } else {
+      memcpy(ctrl, p->last_ctrl, sizeof ctrl);
+    }
+    for (int j = 0; j < 8; j++) {
+      const double lo = m->act_ctrlrange[2 * (1 + j)], hi = m->act_ctrlrange[2 * (1 + j) + 1];
+      arm_ctrl[8 * i + j] = ctrl[j] < lo ? lo : (ctrl[j] > hi ? hi : ctrl[j]);
+    }
+    for (int j = 0; j < A; j++)
+      if (j != i) ik[j].ignore[i] = p->target;
+  }
+}
+
+static int env_ik_solve(void* ctx, int arm, const double* tp, const double* tq, double* q7) {
+  or_env* e = ctx;
+  int steps = 0;
+  int ok = or_ik_solve(e->m, e->ik_d, e->d->qpos, arm, tp, tq, q7, &steps);
+  e->ik_steps += steps;
+  return ok;
+}
+
+static void ik_compose(or_env* e, double* arm_ctrl) {
+  const or_model* m = e->m;
+  double grip[3 * OR_IK_MAXA], base[3 * OR_IK_MAXA];
+  for (int i = 0; i < m->A; i++) {
+    memcpy(grip + 3 * i, e->d->site_xpos + 3 * m->grip_site[i], 3 * sizeof(double));
+    memcpy(base + 3 * i, e->d->site_xpos + 3 * m->base_site[i], 3 * sizeof(double));
+  }
+  e->ik_steps = 0;
+  or_ik_compose(m, e->ik, e->d->qpos, e->d->qvel, grip, base, e->t.in_scene, e->t.n_in, env_ik_solve, e, arm_ctrl);
+  for (int i = 0; i < m->A; i++)
+    for (int o = 0; o < m->A; o++) e->t.ik_ignore[i][o] = e->ik[i].ignore[o];
+}
+
+/* _process_action of one arm's 8 action entries (environments.py:84-102) */
+static void process8(const or_model* m, const float* a, double* out) {
+  for (int j = 0; j < 8; j++) {
+    float th = (float)tanh((double)a[j]);
+    float s = (th + 1.0f) * 0.5f;
+    double lo = m->act_ctrlrange[2 * (1 + j)], hi = m->act_ctrlrange[2 * (1 + j) + 1];
+    out[j] = lo + (double)s * (hi - lo);
+  }
+}
+
+/* _compose_control of the env class (environments.py:104-127, 405-420, 442-459, 481-495, 517-535,
+ * 594-612, 628-645) -> the A arm commands handed to step_sim.  `ik` = the IK proposals of this compose
+ * (non-toggle IK classes, already computed by or_ik_compose), `ik_state` = the policies' states after it;
+ * toggles read the proposals of the last observation and update pause_last. */
+void or_compose_class(const or_model* m, int env_class, const float* action, const double* ik, const int* ik_state,
+                      const double* ik_actions /* 8A */, double* pause_last /* 8A */, double* arm_ctrl) {
+  const int A = m->A;
+  double pa[8];
+  switch (env_class) {
+    case OR_ENV_ALLFULLRL:
+      or_task_process_action(m, action, arm_ctrl);
+      break;
+    case OR_ENV_FACTORY:
+      memcpy(arm_ctrl, ik, 8 * A * sizeof(double));
+      break;
+    case OR_ENV_SINGLEFULLRL:
+      memcpy(arm_ctrl, ik, 8 * A * sizeof(double));
+      process8(m, action, arm_ctrl);
+      break;
+    case OR_ENV_SINGLEDELTA:
+      memcpy(arm_ctrl, ik, 8 * A * sizeof(double));
+      if (ik_state[0] != OR_IK_IDLE) {
+        process8(m, action, pa);
+        for (int j = 0; j < 8; j++) arm_ctrl[j] += 0.5 * pa[j];
+      }
+      break;
+    case OR_ENV_ALLDELTA:
+      memcpy(arm_ctrl, ik, 8 * A * sizeof(double));
+      for (int i = 0; i < A; i++)
+        if (ik_state[i] != OR_IK_IDLE) {
+          process8(m, action + 8 * i, pa);
+          for (int j = 0; j < 8; j++) arm_ctrl[8 * i + j] += 0.5 * pa[j];
+        }
+      break;
+    case OR_ENV_PAUSE_TOGGLE:
+      for (int i = 0; i < A; i++)
+        memcpy(arm_ctrl + 8 * i, action[i] == 1.0f ? ik_actions + 8 * i : pause_last + 8 * i, 8 * sizeof(double));
+      memcpy(pause_last, arm_ctrl, 8 * A * sizeof(double));
+      break;
+    case OR_ENV_BACKUP_TOGGLE:
+      for (int i = 0; i < A; i++)
+        memcpy(arm_ctrl + 8 * i, action[i] == 1.0f ? ik_actions + 8 * i : OR_IK_DEFAULT_POSE, 8 * sizeof(double));
+      break;
+  }
+}
+
+static void compose(or_env* e, const float* action, double* arm_ctrl) {
+  const int A = e->m->A;
+  double ik[8 * OR_IK_MAXA], ika[8 * OR_IK_MAXA], pl[8 * OR_IK_MAXA];
+  int st[OR_IK_MAXA];
+  const int c = e->env_class;
+  if (c != OR_ENV_ALLFULLRL && !is_toggle(c)) ik_compose(e, ik);
+  for (int i = 0; i < A; i++) {
+    st[i] = e->ik[i].state;
+    memcpy(ika + 8 * i, e->ik_actions[i], 8 * sizeof(double));
+    memcpy(pl + 8 * i, e->pause_last[i], 8 * sizeof(double));
+  }
+  or_compose_class(e->m, c, action, ik, st, ika, pl, arm_ctrl);
+  for (int i = 0; i < A; i++) memcpy(e->pause_last[i], pl + 8 * i, 8 * sizeof(double));
+}
+
+/* _process_observation (environments.py:55-82), IKTogglingEnv adds the proposals of a fresh
+ * FactoryManipulationEnv._compose_control (environments.py:560-577) */
+static void env_obs(or_env* e, float* obs) {
+  if (is_toggle(e->env_class)) {
+    double prop[8 * OR_IK_MAXA];
+    ik_compose(e, prop);
+    for (int i = 0; i < e->m->A; i++) memcpy(e->ik_actions[i], prop + 8 * i, 8 * sizeof(double));
+  }
+  if (!obs) return;
+  or_task_obs(&e->t, e->m, e->d->qpos, e->d->qvel, obs);
+  if (is_toggle(e->env_class)) {
+    float* o = obs + 24 * e->m->A + 13 * e->m->K;
+    for (int i = 0; i < e->m->A; i++)
+      for (int j = 0; j < 8; j++) o[8 * i + j] = (float)e->ik_actions[i][j];
+  }
+}
+
 void or_env_free(or_env* e) {
   if (!e) return;
   or_data_free(e->d);
+  or_data_free(e->ik_d);
   or_model_free(e->m);
   free(e->stage_qpos);
   free(e->stage_qvel);
@@ -328,7 +502,8 @@ void or_env_reset(or_env* e, float* obs) {
   memcpy(e->stage_qvel, e->d->qvel, e->m->nv * sizeof(double));
   e->ep_return = 0;
   e->ep_len = 0;
-  if (obs) or_task_obs(&e->t, e->m, e->d->qpos, e->d->qvel, obs);
+  for (int i = 0; i < e->m->A; i++) or_ik_arm_reset(&e->ik[i]); /* environments.py:243-244 */
+  env_obs(e, obs);
 }
 
 int or_env_step(or_env* e, const float* action, float* obs, double* reward, double* info) {
@@ -336,7 +511,7 @@ int or_env_step(or_env* e, const float* action, float* obs, double* reward, doub
   or_data* d = e->d;
   or_task* t = &e->t;
   double arm_ctrl[128], ctrl[128];
-  or_task_process_action(m, action, arm_ctrl);
+  compose(e, action, arm_ctrl);
   or_task_clip_ctrl(t, m, arm_ctrl, ctrl);
   int force_term = 0;
   for (int s = 0; s < t->frame_skip; s++) {
@@ -366,7 +541,7 @@ int or_env_step(or_env* e, const float* action, float* obs, double* reward, doub
   *reward = or_task_reward(t, m, d->qpos, grip, action);
   e->ep_return += *reward;
   e->ep_len++;
-  if (obs) or_task_obs(t, m, d->qpos, d->qvel, obs);
+  env_obs(e, obs);
   if (info) {
     info[0] = t->scores[0];
     info[1] = t->scores[1];

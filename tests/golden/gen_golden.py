@@ -373,15 +373,41 @@ class FakePhysics:
             self.script(self)
 
     def copy(self, share_model=True):
-        return self
+        # physics.copy(share_model=True) (ik_policy.py:270): a separate data block, the model shared
+        return _PhysicsCopy(self)
+
+
+class _PhysicsCopy:
+    def __init__(self, p):
+        self.lay = p.lay
+        self.data = types.SimpleNamespace(qpos=p.data.qpos.copy(), qvel=p.data.qvel.copy())
+        lay = p.lay
+        data = self.data
+
+        class QI:
+            def __getitem__(s, names):
+                if isinstance(names, str):
+                    return data.qpos[lay["qadr"][names]]
+                return data.qpos[[lay["qadr"][n] for n in names]]
+
+        self.named = types.SimpleNamespace(data=types.SimpleNamespace(qpos=QI()))
+
+
+FAKE_IK_CALLS = []
 
 
 def fake_ik(physics, site, target_pos, target_quat, joint_names, max_steps=10):
-    # deterministic, non-physical stand-in for dm_control IK (IK numerics are parity-unpinned)
+    # deterministic, non-physical stand-in for dm_control IK (IK numerics are parity-unpinned); the
+    # success flag varies with the target so both branches of ik_policy.py:266-282 are exercised
     q = np.zeros(physics.lay["nq"])
     for n, j in enumerate(joint_names):
         q[physics.lay["qadr"][j]] = np.tanh(target_pos[n % 3] + 0.1 * n)
-    return types.SimpleNamespace(success=bool(target_pos[2] < 5.0), qpos=q, steps=1)
+    ok = bool(target_pos[2] < 5.0) and int(abs(float(target_pos[0])) * 1e4) % 5 != 0
+    arm = int(site.split("/")[0].replace("arm", ""))
+    FAKE_IK_CALLS.append(dict(arm=arm, target_pos=np.array(target_pos, dtype=np.float64),
+                              target_quat=np.array(target_quat, dtype=np.float64), success=ok,
+                              q7=np.array([q[physics.lay["qadr"][j]] for j in joint_names])))
+    return types.SimpleNamespace(success=ok, qpos=q, steps=1)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -566,6 +592,231 @@ def gen_episodes(env_cls_name, A, K, seed, n_steps, events, reward_kw, tag, act_
     return meta
 
 
+# ----------------------------------------------------------------------------------------------
+# IK base policy episodes (ik_policy.py + the IK env classes of environments.py)
+# ----------------------------------------------------------------------------------------------
+IK_STATE_NAMES = ["IDLE", "GO_TO_GRASP", "GRASP_APPROACH", "GRASP_CLOSE", "POST_GRASP", "GO_TO_RELEASE", "RELEASE"]
+
+
+def _cube_idx(obj):
+    return -1 if obj is None else int(obj.parent.attrs["model"].replace("cube", ""))
+
+
+def make_ik_script(rng, A, K, lay):
+    """cooperative fake physics: arms track their last command, grippers land near their last IK target,
+    grasped cubes follow the gripper, released cubes drop into the bucket -- so every FSM edge is taken"""
+    arm_rng = np.array([2.96706, 2.0944, 2.96706, 2.0944, 2.96706, 2.0944, 3.05433])
+    bpos = bucket_pos(A)
+    step = {"n": 0}
+
+    def script(p):
+        step["n"] += 1
+        env = ENV_REF["env"]
+        tm = env.task_manager
+        q, v = p.data.qpos, p.data.qvel
+        last_target = ENV_REF.setdefault("last_target", {})
+        for c in FAKE_IK_CALLS:
+            last_target[c["arm"]] = c["target_pos"]
+        for i in range(A):
+            a = 1 + 7 * K + 9 * i
+            b = 1 + 6 * K + 9 * i
+            cmd = p._last_ctrl[1 + 8 * i:1 + 8 * i + 7]
+            if rng.random() < 0.85:
+                q[a:a + 7] = cmd + rng.normal(0, 0.03, 7)
+            else:
+                q[a:a + 7] = rng.uniform(-1, 1, 7) * arm_rng
+            q[a + 7:a + 9] = rng.uniform(0.0, 0.06, 2)
+            v[b:b + 9] = rng.normal(0, 0.3, 9)
+            base = p.sites[f"arm{i}/player_site"]
+            holding = env.ik_policies[i].state.name in ("GRASP_CLOSE", "POST_GRASP", "GO_TO_RELEASE")
+            if i in last_target and rng.random() < (0.97 if holding else 0.85):
+                site = last_target[i] + rng.normal(0, 0.015, 3)
+            else:  # somewhere in the arm's workspace, inside the TaskManager bounds (|x| <= 1.2)
+                site = base + rng.uniform(-0.45, 0.45, 3) * np.array([1, 1, 0.6]) + np.array([0, 0, 0.5])
+            p.sites[f"arm{i}/iiwa14/single_gripper/between_gripper_plates"] = site
+        q[0] -= 0.01
+        v[0] = -0.1
+        holders = {}
+        for i, pol in enumerate(env.ik_policies):
+            k = _cube_idx(pol.target_object)
+            if k >= 0:
+                holders[k] = (i, pol.state.name)
+        for o in tm._in_scene:
+            k = _cube_idx(o)
+            a = 1 + 7 * k
+            b = 1 + 6 * k
+            if q[a + 2] > 1.5:  # just spawned: land on the belt
+                q[a:a + 3] = [rng.normal(0, 0.05), 1.0 - rng.uniform(0, 0.05), 1.13 + rng.uniform(0, 0.01)]
+            else:
+                q[a + 1] -= rng.uniform(0.02, 0.06)
+                q[a] += rng.normal(0, 0.01)
+            qq = rng.normal(0, 1, 4)
+            q[a + 3:a + 7] = qq / np.linalg.norm(qq)
+            v[b:b + 6] = rng.normal(0, 0.1, 6)
+            if k in holders:
+                i, st = holders[k]
+                grip = p.sites[f"arm{i}/iiwa14/single_gripper/between_gripper_plates"]
+                if st in ("GRASP_APPROACH", "GRASP_CLOSE", "POST_GRASP", "GO_TO_RELEASE") and rng.random() < 0.96:
+                    q[a:a + 3] = grip + rng.normal(0, 0.01, 3)
+                elif st == "RELEASE" and rng.random() < 0.5:
+                    q[a:a + 3] = bpos[i % 2] + np.array([0.0, 0.0, 0.05])
+        geoms, forces = [], []
+        if step["n"] % 97 == 0:  # an occasional force termination -> reset coverage
+            geoms.append((3, 13 + K + 70 * (step["n"] % A) + 30))
+            forces.append(np.array([250.0, 0, 0, 0, 0, 0]))
+        p.data.ncon = len(geoms)
+        p.data.contact = _Contacts(geoms)
+        p.forces = forces
+
+    return script
+
+
+def gen_ik_episodes(env_cls_name, A, K, seed, n_steps, tag, act_seed=0):
+    """act()-level and compose-level records of the reference's IKPolicy under a fake IK solver"""
+    import environments as envs_mod
+    import challenge_env.ik_policy as ikp
+
+    rng = np.random.default_rng(2000 + seed + 17 * A + K)
+    lay = layout(A, K)
+    FakePhysics.current = FakePhysics(A, K, make_ik_script(rng, A, K, lay))
+    phys = FakePhysics.current
+    phys._last_ctrl = np.zeros(lay["nu"])
+    ENV_REF.pop("last_target", None)
+    acts, comps = [], []
+    cur = {"step": -1, "compose": -1}
+
+    def snap(pol):
+        ign = [-1] * A
+        for owner, obj in pol.ignore_objects.items():
+            ign[owner] = _cube_idx(obj)
+        ms = pol._move_start_pos
+        return dict(state=int(pol.state.value), counter=int(pol.state_counter), target=_cube_idx(pol.target_object),
+                    ignore=ign, last_ctrl=np.array(pol.last_ctrl, dtype=np.float64),
+                    move_start=np.zeros(3) if ms is None else np.array(ms, dtype=np.float64))
+
+    orig_act = ikp.IKPolicy.act
+
+    def rec_act(self):
+        env = ENV_REF["env"]
+        before = snap(self)
+        n0 = len(FAKE_IK_CALLS)
+        out = orig_act(self)
+        calls = FAKE_IK_CALLS[n0:]
+        acts.append(dict(step=cur["step"], compose=cur["compose"], arm=self.arm_id, before=before, after=snap(self),
+                         ctrl=np.array(out, dtype=np.float64), calls=calls))
+        return out
+
+    ikp.IKPolicy.act = rec_act
+    orig_compose = envs_mod.FactoryManipulationEnv._compose_control
+
+    def rec_compose(self, action):
+        # record the IK compose: FactoryManipulationEnv's own (step passes the action) or an override's super()
+        # call (passes None); AllFullRL-style overrides never get here
+        if action is not None and type(self)._compose_control is not rec_compose:
+            return orig_compose(self, action)
+        cur["compose"] += 1
+        tm = self.task_manager
+        p = self.physics
+        rec = dict(step=cur["step"], compose=cur["compose"], qpos=p.data.qpos.copy(), qvel=p.data.qvel.copy(),
+                   grip=np.stack([p.sites[f"arm{i}/iiwa14/single_gripper/between_gripper_plates"].copy()
+                                  for i in range(A)]),
+                   base=np.stack([p.sites[f"arm{i}/player_site"].copy() for i in range(A)]),
+                   in_scene=[_cube_idx(o) for o in tm._in_scene],
+                   before=[snap(pol) for pol in self.ik_policies])
+        out = orig_compose(self, action)
+        rec["after"] = [snap(pol) for pol in self.ik_policies]
+        rec["arm_ctrl"] = np.concatenate([np.asarray(x, dtype=np.float64) for x in out])
+        comps.append(rec)
+        return out
+
+    envs_mod.FactoryManipulationEnv._compose_control = rec_compose
+    cls = getattr(envs_mod, env_cls_name)
+    prog = dict(gripper_to_closest_cube_reward_factor=0.2, closest_cube_to_bucket_reward_factor=0.4,
+                small_action_norm_reward_factor=0.3, base_reward=0.4)
+    kw = dict(num_arms=A, max_num_objects=K, seed=seed, render_mode="rgb_array")
+    if issubclass(cls, envs_mod.ProgressRewardEnv):
+        kw.update(prog)
+    env = cls(**kw)
+    ENV_REF["env"] = env
+    orig_set = phys.set_control
+
+    def set_control(ctrl):
+        orig_set(ctrl)
+        phys._last_ctrl = np.array(ctrl, dtype=np.float64)
+
+    phys.set_control = set_control
+    sent = []
+    orig_unscaled = env._step_sim_unscaled
+
+    def rec_unscaled(ctrl):
+        sent.append(np.array(ctrl, dtype=np.float64))
+        return orig_unscaled(ctrl)
+
+    env._step_sim_unscaled = rec_unscaled
+    arng = np.random.default_rng(act_seed)
+    steps = []
+    obs, _ = env.reset()
+    obs0 = np.asarray(obs, dtype=np.float64)
+    for t in range(n_steps):
+        cur["step"] = t
+        if env_cls_name.endswith("ToggleEnv"):
+            action = arng.integers(0, 2, A)
+        else:
+            action = arng.uniform(-2, 2, env.action_space.shape[0]).astype(np.float32)
+        obs, reward, term, trunc, info = env.step(action)
+        steps.append(dict(action=np.asarray(action, dtype=np.float64), obs=np.asarray(obs, dtype=np.float64),
+                          reward=float(reward), terminated=bool(term), scores=list(info["scores"]),
+                          sent=sent[-1][1:].copy(), post_qpos=phys.data.qpos.copy(),
+                          post_grip=np.stack([phys.sites[f"arm{i}/iiwa14/single_gripper/between_gripper_plates"].copy()
+                                              for i in range(A)]),
+                          post_in_scene=[_cube_idx(o) for o in env.task_manager._in_scene] +
+                          [-1] * (K - len(env.task_manager._in_scene))))
+        if term:
+            cur["step"] = t + 0.5
+            env.reset()
+    ikp.IKPolicy.act = orig_act
+    envs_mod.FactoryManipulationEnv._compose_control = orig_compose
+    # flatten to arrays
+    out = {"A": A, "K": K, "seed": seed, "obs0": obs0}
+    for key in ["action", "obs", "reward", "terminated", "scores", "sent", "post_qpos", "post_grip", "post_in_scene"]:
+        out[f"step_{key}"] = np.asarray([s[key] for s in steps])
+    def arm_arrays(prefix, recs):
+        out[f"{prefix}_i"] = np.asarray([[r["state"], r["counter"], r["target"]] + r["ignore"] for r in recs], np.int32)
+        out[f"{prefix}_d"] = np.asarray([np.concatenate([r["last_ctrl"], r["move_start"]]) for r in recs])
+    arm_arrays("act_before", [a["before"] for a in acts])
+    arm_arrays("act_after", [a["after"] for a in acts])
+    out["act_meta"] = np.asarray([[a["step"] * 2, a["compose"], a["arm"], len(a["calls"])] for a in acts], np.int64)
+    out["act_ctrl"] = np.asarray([a["ctrl"] for a in acts])
+    out["act_call_args"] = np.asarray([np.concatenate([a["calls"][0]["target_pos"], a["calls"][0]["target_quat"]])
+                                       if a["calls"] else np.full(7, np.nan) for a in acts])
+    out["act_call_result"] = np.asarray([np.concatenate([[float(a["calls"][0]["success"])], a["calls"][0]["q7"]])
+                                         if a["calls"] else np.full(8, np.nan) for a in acts])
+    # inputs of each act = its compose's physics snapshot
+    out["comp_meta"] = np.asarray([[c["step"] * 2, c["compose"], len(c["in_scene"])] for c in comps], np.int64)
+    out["comp_qpos"] = np.asarray([c["qpos"] for c in comps])
+    out["comp_qvel"] = np.asarray([c["qvel"] for c in comps])
+    out["comp_grip"] = np.asarray([c["grip"] for c in comps])
+    out["comp_base"] = np.asarray([c["base"] for c in comps])
+    out["comp_in_scene"] = np.asarray([c["in_scene"] + [-1] * (K - len(c["in_scene"])) for c in comps], np.int32)
+    out["comp_arm_ctrl"] = np.asarray([c["arm_ctrl"] for c in comps])
+    for which in ["before", "after"]:
+        recs = [r for c in comps for r in c[which]]
+        out[f"comp_{which}_i"] = np.asarray([[r["state"], r["counter"], r["target"]] + r["ignore"] for r in recs],
+                                            np.int32).reshape(len(comps), A, -1)
+        out[f"comp_{which}_d"] = np.asarray([np.concatenate([r["last_ctrl"], r["move_start"]]) for r in recs]
+                                            ).reshape(len(comps), A, -1)
+    np.savez_compressed(os.path.join(OUT, f"ik_{tag}.npz"), **out)
+    hist = {}
+    for a in acts:
+        n = IK_STATE_NAMES[a["after"]["state"]]
+        hist[n] = hist.get(n, 0) + 1
+    return {"env_class": env_cls_name, "A": A, "K": K, "seed": seed, "n_steps": n_steps, "acts": len(acts),
+            "composes": len(comps), "ik_calls": int(sum(len(a["calls"]) for a in acts)),
+            "ik_success": int(sum(c["success"] for a in acts for c in a["calls"])),
+            "episodes": int(sum(s["terminated"] for s in steps)), "states_after_act": hist,
+            "scores_final": steps[-1]["scores"]}
+
+
 def gen_rng_vectors():
     """PCG64/SeedSequence draws as the reference consumes them (scene.py:121-131, task_utils.py:47-52)."""
     out = {}
@@ -619,7 +870,23 @@ def gen_scene_draws():
     return res
 
 
-def main():
+def main_ik():
+    """IK fixtures only (ik_*.npz + ik_meta.json); the task-layer fixtures stay as they are"""
+    meta = {"generator": "tests/golden/gen_golden.py --ik", "reference": "nkirschi/Factory-MARL @ 2024-12-20",
+            "numpy": np.__version__, "fixtures": {}}
+    for cls, A, K, seed, n, tag, aseed in [("FactoryManipulationEnv", 2, 4, 42, 400, "factory_2x4", 0),
+                                           ("PauseIKToggleEnv", 4, 16, 42, 300, "pause_4x16", 1),
+                                           ("BackupIKToggleEnv", 2, 8, 7, 300, "backup_2x8", 2),
+                                           ("SingleDeltaProgressRewardEnv", 2, 4, 42, 300, "singledelta_2x4", 3),
+                                           ("AllDeltaProgressRewardEnv", 2, 6, 5, 300, "alldelta_2x6", 4),
+                                           ("SingleFullRLProgressRewardEnv", 2, 4, 9, 300, "singlefull_2x4", 5)]:
+        meta["fixtures"][tag] = gen_ik_episodes(cls, A, K, seed, n, tag, act_seed=aseed)
+        print(tag, json.dumps(meta["fixtures"][tag]))
+    with open(os.path.join(OUT, "ik_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+def _setup():
     sys.path.insert(0, os.path.join(REF, "challenge_env"))
     sys.path.insert(0, os.path.join(REF, "src"))
     _install_stubs()
@@ -635,6 +902,9 @@ def main():
 
     tu.TaskManager.__init__ = tm_init
 
+
+def main():
+    _setup()
     meta = {"generator": "tests/golden/gen_golden.py", "reference": "nkirschi/Factory-MARL @ 2024-12-20",
             "numpy": np.__version__, "fixtures": {}}
     np.savez_compressed(os.path.join(OUT, "rng_pcg64.npz"), **gen_rng_vectors())
@@ -675,4 +945,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--ik" in sys.argv:
+        _setup()
+        main_ik()
+    else:
+        main()

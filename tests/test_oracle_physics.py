@@ -292,3 +292,23 @@ def test_impedance_curve(oracle):
     # power 2 below the midpoint: d = dmin + (x/mid)^2*mid * (dmax - dmin)
     x = 0.00025
     assert abs(f(-x) - (0.9 + (x / 0.001) ** 2 / 0.5 * 0.05)) < 1e-15
+
+
+def test_ik_base_policy_scores_end_to_end(oracle):
+    """system-level known answer: FactoryManipulationEnv (every arm on the IK base policy, ik_policy.py) over
+    the oracle's own physics, kinematics and DLS IK picks cubes off the belt and drops them into the buckets
+    -- the behaviour the reference's base policy exists for.  Measured: 5 cubes scored (3 + 2) in 300
+    env-steps from reset, both arms scoring, every FSM state visited."""
+    import numpy as np
+
+    e = oracle.Env(2, 4, 42, env_class="FactoryManipulationEnv")
+    e.reset()
+    seen = set()
+    total = 0.0
+    for _ in range(300):
+        _, r, term, _, info = e.step(np.zeros(0, np.float32))
+        total += r
+        seen |= {e.ik_arm(i)["state"] for i in range(2)}
+        assert not term
+    assert info["scores"][0] >= 2 and info["scores"][1] >= 1 and total == sum(info["scores"])
+    assert seen == set(range(7))
