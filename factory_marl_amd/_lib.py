@@ -9,8 +9,14 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTORYSIM_LIB", os.path.join(_HERE, "libfactorysim.so"))
 
-FM_ENV_FACTORY_SCORE = 0
+# env classes (include/factorysim.h FM_ENV_*)
+FM_ENV_FACTORY = 0
 FM_ENV_ALLFULLRL_PROGRESS = 1
+FM_ENV_SINGLEFULLRL_PROGRESS = 2
+FM_ENV_SINGLEDELTA_PROGRESS = 3
+FM_ENV_ALLDELTA_PROGRESS = 4
+FM_ENV_PAUSE_IK_TOGGLE = 5
+FM_ENV_BACKUP_IK_TOGGLE = 6
 FM_FP32 = 0
 FM_FP64 = 1
 

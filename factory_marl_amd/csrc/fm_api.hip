@@ -48,6 +48,8 @@ struct fm_handle {
   std::vector<void*> allocs;
   // device model arrays (typed by precision, stored as void*)
   void* arm_base = nullptr;
+  double* ctrlrange_d = nullptr;
+  double* arm_base_w = nullptr;
   void* body = nullptr;
   void* dof = nullptr;
   void* ctrlrange = nullptr;
@@ -128,9 +130,11 @@ static Model<T> make_model(const fm_handle* h) {
   M.solver_iter = c.solver_iterations;
   M.solver_tol = c.solver_tolerance;
   M.arm_base = (const T*)h->arm_base;
+  M.arm_base_w = h->arm_base_w;
   M.body = (const T*)h->body;
   M.dof = (const T*)h->dof;
   M.ctrlrange = (const T*)h->ctrlrange;
+  M.ctrlrange_d = h->ctrlrange_d;
   M.geom = (const T*)h->geom;
   M.geom_i = h->geom_i;
   M.pair = h->pair;
@@ -224,9 +228,16 @@ static int create_typed(fm_handle* h) {
   }
   int r;
   if ((r = upload<T>(h, &h->arm_base, arm_base))) return r;
+  {
+    std::vector<double> bw(12 * s.A);
+    for (int i = 0; i < s.A; i++)
+      for (int k = 0; k < 12; k++) bw[12 * i + k] = s.arm_base[i][k];
+    if ((r = upload_raw<double>(h, &h->arm_base_w, bw))) return r;
+  }
   if ((r = upload<T>(h, &h->body, body))) return r;
   if ((r = upload<T>(h, &h->dof, dof))) return r;
   if ((r = upload<T>(h, &h->ctrlrange, ctrl))) return r;
+  if ((r = upload_raw<double>(h, &h->ctrlrange_d, ctrl))) return r;
   if ((r = upload<T>(h, &h->geom, geom))) return r;
   if ((r = upload_raw<int>(h, &h->geom_i, geom_i))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->pair, s.pairs))) return r;
@@ -270,10 +281,24 @@ static int create_typed(fm_handle* h) {
   HIPCHK(hipMemset(h->phys, 0, N * d.phys_stride * sizeof(double)));
   HIPCHK(hipMalloc((void**)&h->dbl, N * d.dbl_stride * sizeof(double)));
   h->allocs.push_back(h->dbl);
-  HIPCHK(hipMemset(h->dbl, 0, N * d.dbl_stride * sizeof(double)));
   HIPCHK(hipMalloc((void**)&h->ints, N * d.int_stride * sizeof(int32_t)));
   h->allocs.push_back(h->ints);
-  HIPCHK(hipMemset(h->ints, 0, N * d.int_stride * sizeof(int32_t)));
+  {
+    // IKPolicy.__init__ (ik_policy.py:76-81) + PauseIKToggleEnv.last_arm_actions (environments.py:592): idle,
+    // no target, nothing ignored, last_ctrl = default pose; the rest is written by fm_reset
+    std::vector<double> db(N * d.dbl_stride, 0.0);
+    std::vector<int32_t> in(N * d.int_stride, 0);
+    for (size_t n = 0; n < N; n++)
+      for (int i = 0; i < d.A; i++) {
+        double* dd = db.data() + n * d.dbl_stride + d.nu + 4 + 2 * d.A + 27 * i;
+        for (int j = 0; j < 8; j++) dd[j] = IK_DEFAULT_POSE[j];
+        int32_t* ii = in.data() + n * d.int_stride + 2 * d.K + I_NINT + (3 + d.A) * i;
+        ii[2] = -1;
+        for (int o = 0; o < d.A; o++) ii[3 + o] = -1;
+      }
+    HIPCHK(hipMemcpy(h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   if ((r = upload_raw<uint64_t>(h, &h->rng, s.rng_init))) return r;
   HIPCHK(hipMalloc((void**)&h->counters, N * FM_NCTR * sizeof(int64_t)));
   h->allocs.push_back(h->counters);
@@ -418,9 +443,13 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
   h->cfg = *cfg;
   h->device = device;
   h->fp64 = cfg->precision == FM_FP64;
-  if (cfg->env_class != FM_ENV_FACTORY_SCORE && cfg->env_class != FM_ENV_ALLFULLRL_PROGRESS) {
+  if (cfg->env_class < FM_ENV_FACTORY || cfg->env_class > FM_ENV_BACKUP_IK_TOGGLE) {
     delete h;
     return set_err(FM_EINVAL, "unknown env_class");
+  }
+  if (cfg->num_arms > 16) {
+    delete h;
+    return set_err(FM_EINVAL, "num_arms > 16");
   }
   if (h->cfg.solver_tolerance <= 0) h->cfg.solver_tolerance = h->fp64 ? 1e-12 : 1e-7;
   if (h->cfg.solver_iterations <= 0) h->cfg.solver_iterations = 100;
@@ -444,14 +473,20 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
   d.ntree = 1 + s.K + s.A;
   d.ncb = (int)s.cbodies.size();
   d.ncbp = (int)s.cb_pairs.size();
-  d.obs_dim = s.obs_dim;
-  d.act_dim = s.act_dim;
+  {
+    const int ec = cfg->env_class;
+    const bool toggle = ec == FM_ENV_PAUSE_IK_TOGGLE || ec == FM_ENV_BACKUP_IK_TOGGLE;
+    d.obs_dim = 24 * s.A + 13 * s.K + (toggle ? 8 * s.A : 0);  // IKTogglingEnv (environments.py:553)
+    d.act_dim = ec == FM_ENV_FACTORY ? 0
+                : (ec == FM_ENV_SINGLEFULLRL_PROGRESS || ec == FM_ENV_SINGLEDELTA_PROGRESS) ? 8
+                : toggle ? s.A : 8 * s.A;
+  }
   d.frame_skip = (int)((1.0 / cfg->control_frequency) / 0.001);
   d.maxcon = cfg->max_contacts > 0 ? std::min(cfg->max_contacts, MAXCON) : MAXCON;
   d.maxrow = 10 * s.A;
   d.phys_stride = 2 * s.nq + 3 * s.nv;
-  d.dbl_stride = s.nu + 3 + 2 * s.A + 1;
-  d.int_stride = 2 * s.K + I_NINT;
+  d.dbl_stride = s.nu + 3 + 2 * s.A + 1 + 27 * s.A;
+  d.int_stride = 2 * s.K + I_NINT + (3 + s.A) * s.A;
   if (hipSetDevice(device) != hipSuccess) {
     delete h;
     return set_err(FM_EDEVICE, "hipSetDevice failed");
@@ -535,7 +570,7 @@ int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
 int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
             const fm_info* info) {
   if (!h) return set_err(FM_EINVAL, "null handle");
-  if (!actions) return set_err(FM_EINVAL, "actions is NULL");
+  if (!actions && h->dm.act_dim > 0) return set_err(FM_EINVAL, "actions is NULL");
   if (!h->was_reset) return set_err(FM_ESTATE, "fm_step before fm_reset");
   HIPCHK(hipSetDevice(h->device));
   StepIO io;

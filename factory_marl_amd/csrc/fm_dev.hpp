@@ -60,7 +60,9 @@ struct Dims {
   int maxcon, maxrow;
   int phys_stride;  // double: qpos nq | qvel nv | qpos_s nq | qvel_s nv | qacc_ws nv
   int dbl_stride;   // double: ctrl_target nu | spawn_freq | speed | play_time | last_grip A | last_bucket A | ep_return
+                    //         | IK block A x 27 (fm_ik.hpp)
   int int_stride;   // int32:  in_scene K | out_scene K | n_in n_out step since fail hidden score0 score1 last0 last1 ep_len
+                    //         | IK block A x (3 + A)
 };
 
 // indices into the int block after the two lists
@@ -78,10 +80,12 @@ struct Model {
   int env_class, solver_iter;
   double solver_tol;
   // arm template
-  cptr<T> arm_base;  // [A][12]  world pos(3), R(9) of the iiwa frame
+  cptr<T> arm_base;  // [A][12]  world pos(3), R(9) of the iiwa frame (kernel frame: zshift)
+  cptr<double> arm_base_w;  // [A][12] the same in float64, world frame (IK base policy, fm_ik.hpp)
   cptr<T> body;      // [10][32] local pos(3) local R(9) mass ipos(3) iR(9) I(3) invw_t invw_r pad(2)
   cptr<T> dof;       // [9][4]   range lo, hi, dof_invweight0, pad
   cptr<T> ctrlrange; // [nu][2]
+  cptr<double> ctrlrange_d;  // [nu][2] float64 (actuator_ctrlrange as the reference clips with it)
   // geoms (compact, collidable)
   cptr<T> geom;      // [ngc][16]  pos(3) R(9) size(3) rbound
   cptr<int> geom_i;  // [ngc][4]   mjid, type, kbody, box slot
@@ -431,19 +435,20 @@ struct FixedDims {
   static constexpr bool fixed = true;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
-  static constexpr int obs_dim = 24 * A_ + 13 * K_, act_dim = 8 * A_, maxrow = 10 * A_;
-  static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1, int_stride = 2 * K_ + I_NINT;
-  int N, nbox, npair, nparam, frame_skip, maxcon, ncbp;
+  static constexpr int maxrow = 10 * A_;
+  static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
+                       int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
+  int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
   __host__ __device__ FixedDims(const Dims& d)
       : N(d.N), nbox(d.nbox), npair(d.npair), nparam(d.nparam), frame_skip(d.frame_skip), maxcon(d.maxcon),
-        ncbp(d.ncbp) {}
+        ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
     return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXCON, maxrow, ntree, TS);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&
-           d.ntree == ntree && d.obs_dim == obs_dim && d.act_dim == act_dim && d.maxrow == maxrow &&
+           d.ntree == ntree && d.maxrow == maxrow &&
            d.phys_stride == phys_stride && d.dbl_stride == dbl_stride && d.int_stride == int_stride;
   }
 };

@@ -33,6 +33,7 @@
 #include "fm_dev.hpp"
 #include "fm_scene.hpp"
 #include "fm_arm_table.hpp"  // generated (gen_tables.cpp)
+#include "fm_ik.hpp"
 
 #ifndef FM_WS_RUNTIME_LAYOUT
 #define FM_WS_RUNTIME_LAYOUT 0
@@ -2616,7 +2617,7 @@ __device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T, DIM>& 
     // difference ctrl - length is exact, only the force is rounded to the build's precision
     for (int u = LANE; u < dm.nu; u += WAVE) {
       double c = w.ctrl()[u];
-      const double lo = (double)M.ctrlrange[2 * u], hi = (double)M.ctrlrange[2 * u + 1];
+      const double lo = M.ctrlrange_d[2 * u], hi = M.ctrlrange_d[2 * u + 1];
       c = c < lo ? lo : (c > hi ? hi : c);
       // transmission (actuator length / velocity) from the float64 master state: the belt and arm dofs it
       // reads are the stage state's (the TaskManager's teleports only move cubes)
@@ -2846,6 +2847,15 @@ __device__ __forceinline__ void task_reset(const Model<T>& M, double* q, double*
   ts[I_S0] = ts[I_S1] = 0;
   ts[I_LS0] = ts[I_LS1] = 0;
   for (int u = 0; u < dm.nu; u++) ctrl[u] = 0.0;
+  // FactoryManipulationEnv.reset -> IKPolicy.reset -> idle_ctrl (environments.py:243-244, ik_policy.py:120-127);
+  // ignore maps, move_start and PauseIKToggleEnv.last_arm_actions persist
+  for (int i = 0; i < dm.A; i++) {
+    const IkArm p = ik_arm(dm, ti, td, i);
+    p.s[0] = IK_IDLE;
+    p.s[1] = 0;
+    p.s[2] = -1;
+    for (int j = 0; j < 8; j++) p.last_ctrl()[j] = IK_DEFAULT_POSE[j];
+  }
   td[0] = M.spawn_freq0;  // spawn_freq
   td[1] = M.init_speed;   // conveyor speed
   td[2] = 0.0;            // play_time
@@ -2935,18 +2945,21 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
   int32_t* ts = ti + 2 * K;
   int sd = (ts[I_S0] + ts[I_S1]) - (ts[I_LS0] + ts[I_LS1]);
   double rew;
-  if (M.env_class == FM_ENV_FACTORY_SCORE) {
+  if (env_score_reward(M.env_class)) {
     rew = sd;
   } else {
     double gc = 0, bc = 0;
     double* lg = td + 3;
     double* lb = td + 3 + A;
     for (int i = 0; i < A; i++) {
-      if (ts[I_NIN] == 0) continue;
       const T* gp = w.site() + 3 * i;
       double best = 0;
       int bi = -1;
+      const int32_t* ign = ik_arm(dm, ti, td, i).s + 3;  // candidates skip the IK policy's ignore map
       for (int c = 0; c < ts[I_NIN]; c++) {
+        bool skip = false;
+        for (int o = 0; o < A; o++) skip |= ign[o] == ti[c];
+        if (skip) continue;
         const double* qq = w.qd() + 1 + 7 * ti[c];
         double dx = qq[0] - (double)gp[0], dy = qq[1] - (double)gp[1], dz = qq[2] - ((double)gp[2] + zshift<T>());
         double dd = sqrt(dx * dx + dy * dy + dz * dz);
@@ -2955,6 +2968,7 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
           bi = c;
         }
       }
+      if (bi < 0) continue;  // no candidate: (None, last distance, 0) (environments.py:306-307, 334-335)
       gc += lg[i] - best;
       lg[i] = best;
       // closest cube to this arm's bucket
@@ -2966,7 +2980,7 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
       lb[i] = db;
     }
     float ss = 0.0f;
-    for (int i = 0; i < 8 * A; i++)
+    for (int i = 0; i < dm.act_dim; i++)
       if (i % 8 != 7) ss += act[i] * act[i];
     float an = expf(-sqrtf(ss));
     double prog = M.base_reward + M.w_grip * gc + M.w_bucket * bc + M.w_action * (double)an;
@@ -2982,7 +2996,7 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
 }
 
 template <typename T, typename DIM>
-__device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w, const int32_t* ti, float* obs) {
+__device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td, float* obs) {
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
   const double* q = w.qd();  // float64 state cast to float32 (base_env.py:92-109)
@@ -3017,12 +3031,108 @@ __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w
     } else if (e < 24 * A + 7 * K) {
       int k = (e - 24 * A) / 7, c = (e - 24 * A) % 7;
       val = k < n ? (float)q[1 + 7 * idx[k] + c] : 0.0f;
-    } else {
+    } else if (e < 24 * A + 13 * K) {
       int k = (e - 24 * A - 7 * K) / 6, c = (e - 24 * A - 7 * K) % 6;
       val = k < n ? (float)v[1 + 6 * idx[k] + c] : 0.0f;
+    } else {  // IKTogglingEnv: the IK proposals (environments.py:576)
+      const int r = e - 24 * A - 13 * K;
+      val = (float)ik_arm(dm, ti, td, r / 8).ik_actions()[r % 8];
     }
     obs[e] = val;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// IK base policy of one arena (fm_ik.hpp): FactoryManipulationEnv._compose_control
+// ------------------------------------------------------------------------------------------------
+// every arm's proposal (IKPolicy.act() clipped to actuator_ctrlrange[1:9]) into prop[8A], FSM state / ignore
+// maps / last_ctrl / move_start updated in the arena's IK block.  Reads the float64 master state; uses the
+// phase-local H region as scratch (free outside a substep's stage / solve).  Not inlined (it runs a few times
+// per env-step): every pointer it receives is global or LDS -- none into a caller's private frame, which a
+// callee could only reach through the flat scratch aperture.
+__device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const double* ctrlrange_d, int A, int K,
+                                            const double* qd, const double* vd, int32_t* ti, double* td,
+                                            int int_base, int dbl_base, double* scr, double* prop) {
+  // scr per arm (24): grip 3 | tpos 3 | tquat 4 | need | close | pad 2 | q 7 | pad 3
+  struct D {
+    int A, K;
+  } dm{A, K};
+  (void)int_base;
+  (void)dbl_base;
+  if (LANE < A) {
+    double q[7], sR[9];
+    for (int j = 0; j < 7; j++) q[j] = qd[1 + 7 * K + 9 * LANE + j];
+    double sp[3];
+    ik_fk(arm_base_w + 12 * LANE, q, sp, sR, nullptr, nullptr);
+    for (int k = 0; k < 3; k++) scr[24 * LANE + k] = sp[k];
+  }
+  SYNC();
+  if (LANE == 0) {  // act() in arm order: each arm's target selection sees the ignore maps written before it
+    const int n_in = ti[2 * K + I_NIN];
+    for (int i = 0; i < A; i++) {
+      const IkArm p = ik_arm(dm, ti, td, i);
+      double* sc = scr + 24 * i;
+      int cl = 0;
+      double g[3] = {sc[0], sc[1], sc[2]}, tp[3] = {0, 0, 0}, tq[4] = {1, 0, 0, 0};
+      sc[10] = ik_plan(A, i, p, ti, n_in, qd, vd, K, g, arm_base_w + 12 * i, tp, tq, &cl);
+      for (int k = 0; k < 3; k++) sc[3 + k] = tp[k];
+      for (int k = 0; k < 4; k++) sc[6 + k] = tq[k];
+      sc[11] = cl;
+      const int tgt = p.s[2];
+      for (int j = 0; j < A; j++)
+        if (j != i) ik_arm(dm, ti, td, j).s[3 + i] = tgt;  // ik_policies[j].ignore(target, owner i)
+    }
+  }
+  FULL_SYNC();
+  if (LANE < A) {
+    const IkArm p = ik_arm(dm, ti, td, LANE);
+    double* sc = scr + 24 * LANE;
+    double ctrl[8];
+    bool ok = false;
+    if (sc[10] != 0.0) {
+      double* q = sc + 14;  // the arm's private copy of its hinges (qpos_from_site_pose, inplace=False), in LDS
+      for (int j = 0; j < 7; j++) q[j] = qd[1 + 7 * K + 9 * LANE + j];
+      ok = ik_solve(arm_base_w + 12 * LANE, q, sc + 3, sc + 6) != 0;
+      if (ok) {
+        for (int j = 0; j < 7; j++) ctrl[j] = q[j];
+        ctrl[7] = sc[11] != 0.0 ? 0.0 : 2.0;
+        for (int j = 0; j < 8; j++) p.last_ctrl()[j] = ctrl[j];
+      }
+    }
+    if (!ok)
+      for (int j = 0; j < 8; j++) ctrl[j] = p.last_ctrl()[j];
+    for (int j = 0; j < 8; j++) {
+      const double lo = ctrlrange_d[2 * (1 + j)], hi = ctrlrange_d[2 * (1 + j) + 1];
+      prop[8 * LANE + j] = ctrl[j] < lo ? lo : (ctrl[j] > hi ? hi : ctrl[j]);
+    }
+  }
+  FULL_SYNC();
+}
+
+template <typename T, typename DIM>
+__device__ __forceinline__ void ik_compose(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td, double* prop) {
+  const DIM dm(M.dm);
+  ik_compose_raw(M.arm_base_w, M.ctrlrange_d, dm.A, dm.K, w.qd(), w.vd(), ti, td, 0, 0, (double*)w.H(), prop);
+}
+
+// IKTogglingEnv._process_observation (environments.py:560-577): fresh proposals, kept for the next step's
+// composition and appended to the observation
+template <typename T, typename DIM>
+__device__ __forceinline__ void ik_proposals(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td) {
+  const DIM dm(M.dm);
+  double* prop = (double*)w.H() + 24 * dm.A;
+  ik_compose(M, w, ti, td, prop);
+  for (int e = LANE; e < 8 * dm.A; e += WAVE) ik_arm(dm, ti, td, e / 8).ik_actions()[e % 8] = prop[e];
+  FULL_SYNC();
+}
+
+// _process_action of one entry (environments.py:84-102): float32 tanh, float64 range
+template <typename T>
+__device__ __forceinline__ double process_action(const Model<T>& M, float a, int j) {
+  const float th = (float)tanh((double)a);  // correctly rounded float32 tanh (np.tanh on float32)
+  const float s = (th + 1.0f) * 0.5f;
+  const double lo = M.ctrlrange_d[2 * (1 + j)], hi = M.ctrlrange_d[2 * (1 + j) + 1];
+  return lo + (double)s * (hi - lo);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3126,7 +3236,8 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   }
   SYNC();
   FULL_SYNC();
-  if (obs) write_obs(M, w, ti, obs + (size_t)arena * dm.obs_dim);
+  if (env_toggle(M.env_class)) ik_proposals(M, w, ti, td);  // reset()'s observation (environments.py:245)
+  if (obs) write_obs(M, w, ti, td, obs + (size_t)arena * dm.obs_dim);
 }
 
 template <typename T, typename DIM>
@@ -3156,24 +3267,54 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
 #define rng (S.rng + 4 * (size_t)arena)
 #define ctr (S.counters + FM_NCTR * (size_t)arena)
 #define act (io.actions + (size_t)arena * dm.act_dim)
-  // ---- ctrl_target (double) and the clipped AllFullRL control (environments.py:84-102, base_env.py:255-262)
+  // ---- ctrl_target (double) and the env class's control (environments.py _compose_control, base_env.py:255-262)
 #define ctrl_ (w.ctrl())
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < nu; u += WAVE) ctrl_[u] = dsrc[u];
   const double speed0 = td[1];
+  const int ec = M.env_class;
+  double* prop = (double*)w.H() + 24 * A;  // IK proposals of this step's compose (phase-local scratch)
+  if (env_ik_at_step(ec)) {  // IKPolicy.act() on the state the step starts from
+    load_state(M, S, w, arena, false);
+    SYNC();
+    ik_compose(M, w, ti, td, prop);
+  }
 #define uctl_ (w.uctl())
   for (int u = LANE; u < nu; u += WAVE) {
     double c;
     if (u == 0) {
       c = speed0;
     } else {
-      int j = (u - 1) % 8;
-      float a = (float)tanh((double)act[u - 1]);  // correctly rounded float32 tanh (np.tanh on float32)
-      float s = (a + 1.0f) * 0.5f;
-      double lo = (double)M.ctrlrange[2 * (1 + j)], hi = (double)M.ctrlrange[2 * (1 + j) + 1];
-      c = lo + (double)s * (hi - lo);
+      const int arm = (u - 1) / 8, j = (u - 1) % 8;
+      switch (ec) {
+        case FM_ENV_ALLFULLRL_PROGRESS:
+          c = process_action(M, act[u - 1], j);
+          break;
+        case FM_ENV_SINGLEFULLRL_PROGRESS:
+          c = arm == 0 ? process_action(M, act[j], j) : prop[u - 1];
+          break;
+        case FM_ENV_SINGLEDELTA_PROGRESS:
+          c = prop[u - 1];
+          if (arm == 0 && ik_arm(dm, ti, td, 0).s[0] != IK_IDLE) c += 0.5 * process_action(M, act[j], j);
+          break;
+        case FM_ENV_ALLDELTA_PROGRESS:
+          c = prop[u - 1];
+          if (ik_arm(dm, ti, td, arm).s[0] != IK_IDLE) c += 0.5 * process_action(M, act[u - 1], j);
+          break;
+        case FM_ENV_PAUSE_IK_TOGGLE: {
+          const IkArm p = ik_arm(dm, ti, td, arm);
+          c = act[arm] == 1.0f ? p.ik_actions()[j] : p.pause_last()[j];
+          p.pause_last()[j] = c;  // last_arm_actions = arm_actions (environments.py:608-611)
+          break;
+        }
+        case FM_ENV_BACKUP_IK_TOGGLE:
+          c = act[arm] == 1.0f ? ik_arm(dm, ti, td, arm).ik_actions()[j] : IK_DEFAULT_POSE[j];
+          break;
+        default:  // FM_ENV_FACTORY
+          c = prop[u - 1];
+      }
     }
-    double lo = (double)M.ctrlrange[2 * u], hi = (double)M.ctrlrange[2 * u + 1];
+    const double lo = M.ctrlrange_d[2 * u], hi = M.ctrlrange_d[2 * u + 1];
     uctl_[u] = c < lo ? lo : (c > hi ? hi : c);
   }
   init_arena(M, w, arena);
@@ -3254,6 +3395,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     SYNC();
     refresh_copies(M, w);  // the TaskManager's teleports wrote the master state
     SYNC();
+    if (env_toggle(ec)) ik_proposals(M, w, ti, td);  // the step's observation (environments.py:197, 560-577)
     const int term = sc_[1] != 0.0;
     if (LANE == 0) {
       const int s_fail = sc_[2] != 0.0;
@@ -3289,7 +3431,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     // ---- auto-reset (reset_sim, base_env.py:177-198): terminal obs, zero state, TaskManager.reset,
     // then one more pass of this loop = the forward at the reset state that leaves qacc_warmstart
     FULL_SYNC();
-    if (io.terminal_obs) write_obs(M, w, ti, io.terminal_obs + (size_t)arena * dm.obs_dim);
+    if (io.terminal_obs) write_obs(M, w, ti, td, io.terminal_obs + (size_t)arena * dm.obs_dim);
     SYNC();
     for (int i = LANE; i < dm.nq; i += WAVE) w.qd()[i] = 0.0;
     for (int i = LANE; i < dm.nv; i += WAVE) {
@@ -3310,7 +3452,8 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   }
   store_state(M, S, w, arena);
   FULL_SYNC();
-  if (io.obs) write_obs(M, w, ti, io.obs + (size_t)arena * dm.obs_dim);
+  if (reset_pass && env_toggle(ec)) ik_proposals(M, w, ti, td);  // reset()'s observation after the auto-reset
+  if (io.obs) write_obs(M, w, ti, td, io.obs + (size_t)arena * dm.obs_dim);
   PMARK(PH_TAIL);
   if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);
 #undef ctrl_

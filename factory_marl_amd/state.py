@@ -1,17 +1,19 @@
 """Pack / unpack the per-arena state record of fm_get_state / fm_set_state (include/factorysim.h).
 
 Record = float64 [qpos nq | qvel nv | qpos_stage nq | qvel_stage nv | qacc_warmstart nv | ctrl_target nu |
-spawn_freq | conveyor_speed | play_time | last_grip_dist A | last_bucket_dist A | episode_return]
+spawn_freq | conveyor_speed | play_time | last_grip_dist A | last_bucket_dist A | episode_return |
+A x (ik last_ctrl 8 | move_start 3 | ik_actions 8 | pause_last 8)]
 + int32 [in_scene K | out_scene K | n_in n_out step_counter steps_since_spawn failure_counter
-hidden_counter score0 score1 last_score0 last_score1 episode_length] + uint64 [PCG64 state_hi state_lo inc_hi inc_lo].
+hidden_counter score0 score1 last_score0 last_score1 episode_length | A x (ik state counter target ignore[A])]
++ uint64 [PCG64 state_hi state_lo inc_hi inc_lo].
 """
 import numpy as np
 
 
 def sizes(A, K):
     nq, nv, nu = 1 + 7 * K + 9 * A, 1 + 6 * K + 9 * A, 1 + 8 * A
-    nd = 2 * nq + 3 * nv + nu + 3 + 2 * A + 1
-    ni = 2 * K + 11
+    nd = 2 * nq + 3 * nv + nu + 3 + 2 * A + 1 + 27 * A
+    ni = 2 * K + 11 + (3 + A) * A
     return nq, nv, nu, nd, ni
 
 
@@ -45,7 +47,7 @@ def fields(A, K, dbl):
     f = {}
     for name, n in [("qpos", nq), ("qvel", nv), ("qpos_stage", nq), ("qvel_stage", nv), ("qacc_warmstart", nv),
                     ("ctrl_target", nu), ("spawn_freq", 1), ("conveyor_speed", 1), ("play_time", 1),
-                    ("last_grip_dist", A), ("last_bucket_dist", A), ("episode_return", 1)]:
+                    ("last_grip_dist", A), ("last_bucket_dist", A), ("episode_return", 1), ("ik", 27 * A)]:
         f[name] = dbl[o:o + n]
         o += n
     return f

@@ -15,11 +15,17 @@ import numpy as np
 
 from . import _lib
 
+# the env classes of src/environments.py (class hierarchy at environments.py:10-22)
 ENV_CLASSES = {
+    "FactoryManipulationEnv": _lib.FM_ENV_FACTORY,
     "AllFullRLProgressRewardEnv": _lib.FM_ENV_ALLFULLRL_PROGRESS,
-    # score-delta reward of FactoryManipulationEnv._get_reward (environments.py:129-149) with AllFullRL actions
-    "AllFullRLScoreEnv": _lib.FM_ENV_FACTORY_SCORE,
+    "SingleFullRLProgressRewardEnv": _lib.FM_ENV_SINGLEFULLRL_PROGRESS,
+    "SingleDeltaProgressRewardEnv": _lib.FM_ENV_SINGLEDELTA_PROGRESS,
+    "AllDeltaProgressRewardEnv": _lib.FM_ENV_ALLDELTA_PROGRESS,
+    "PauseIKToggleEnv": _lib.FM_ENV_PAUSE_IK_TOGGLE,
+    "BackupIKToggleEnv": _lib.FM_ENV_BACKUP_IK_TOGGLE,
 }
+TOGGLE_CLASSES = ("PauseIKToggleEnv", "BackupIKToggleEnv")
 
 # BaseEnv.__init__ defaults (base_env.py:15-35); ProgressRewardEnv weights of the saved runs
 # (runs/rk5rxnav.json env_kwargs)
@@ -46,6 +52,21 @@ class Box:
 
     def __repr__(self):
         return f"Box({self.low}, {self.high}, {self.shape}, {self.dtype})"
+
+
+class MultiDiscrete:
+    """minimal gymnasium.spaces.MultiDiscrete stand-in (IKTogglingEnv.action_space, environments.py:551)"""
+
+    def __init__(self, nvec):
+        self.nvec = np.asarray(nvec, dtype=np.int64)
+        self.shape = self.nvec.shape
+        self.dtype = np.dtype(np.int64)
+
+    def sample(self, rng=np.random):
+        return rng.integers(0, self.nvec) if hasattr(rng, "integers") else rng.randint(0, self.nvec)
+
+    def __repr__(self):
+        return f"MultiDiscrete({self.nvec})"
 
 
 class FactoryVecEnv:
@@ -95,7 +116,10 @@ class FactoryVecEnv:
         self.obs_dim = L.fm_obs_dim(h)
         self.act_dim = L.fm_act_dim(h)
         self.observation_space = Box(-np.inf, np.inf, (self.obs_dim,), np.float32)
-        self.action_space = Box(-1.0, 1.0, (self.act_dim,), np.float32)
+        if env_class in TOGGLE_CLASSES:
+            self.action_space = MultiDiscrete([2] * self.act_dim)
+        else:
+            self.action_space = Box(-1.0, 1.0, (self.act_dim,), np.float32)
         self.return_numpy = return_numpy
         dev = self.device
         n = self.num_envs
@@ -145,7 +169,11 @@ class FactoryVecEnv:
         a = actions
         if not (self.torch.is_tensor(a) and a.device == self.device and a.dtype == self.torch.float32
                 and a.is_contiguous()):
-            a = self.torch.as_tensor(a, dtype=self.torch.float32, device=self.device).contiguous()
+            # MultiDiscrete int actions (toggle classes) become 0.0 / 1.0
+            a = self.torch.as_tensor(np.asarray(a) if not self.torch.is_tensor(a) else a, device=self.device)
+            a = a.to(self.torch.float32).contiguous()
+        if a.numel() == 0:  # FactoryManipulationEnv: no action entries; the ABI still takes a pointer
+            a = self.torch.zeros(max(self.num_envs, 1), dtype=self.torch.float32, device=self.device)
         self._actions = a
         self._bind_stream()
         _lib.check(self._L.fm_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(self.obs.data_ptr()),

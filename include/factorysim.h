@@ -35,9 +35,19 @@ extern "C" {
 #define FM_ENOMEM (-3)
 #define FM_ESTATE (-4)  /* call order (e.g. step before reset) */
 
-/* env classes (environments.py) whose step() this library implements */
-#define FM_ENV_FACTORY_SCORE 0      /* score-delta reward (FactoryManipulationEnv._get_reward), AllFullRL actions */
-#define FM_ENV_ALLFULLRL_PROGRESS 1 /* AllFullRLProgressRewardEnv (environments.py:462-495) */
+/* env classes of src/environments.py whose step() this library implements.  Actions are float32 [N, act_dim]:
+ *   FACTORY                  act_dim 0  (every arm on the IK base policy; pass any pointer, it is not read)
+ *   SINGLEFULLRL, SINGLEDELTA act_dim 8  (Box[-1, 1])
+ *   ALLFULLRL, ALLDELTA       act_dim 8A (Box[-1, 1])
+ *   PAUSE / BACKUP_IK_TOGGLE  act_dim A  (MultiDiscrete([2] * A) as 0.0 / 1.0; 1.0 = follow the IK proposal)
+ * Observations are 24A + 13K float32 (+ 8A IK proposals for the two toggle classes). */
+#define FM_ENV_FACTORY 0              /* FactoryManipulationEnv: IK on every arm, score-delta reward (environments.py:25-248) */
+#define FM_ENV_ALLFULLRL_PROGRESS 1   /* AllFullRLProgressRewardEnv (environments.py:462-495) */
+#define FM_ENV_SINGLEFULLRL_PROGRESS 2 /* SingleFullRLProgressRewardEnv (environments.py:386-420) */
+#define FM_ENV_SINGLEDELTA_PROGRESS 3 /* SingleDeltaProgressRewardEnv (environments.py:423-459) */
+#define FM_ENV_ALLDELTA_PROGRESS 4    /* AllDeltaProgressRewardEnv (environments.py:498-535) */
+#define FM_ENV_PAUSE_IK_TOGGLE 5      /* PauseIKToggleEnv (environments.py:538-612) */
+#define FM_ENV_BACKUP_IK_TOGGLE 6     /* BackupIKToggleEnv (environments.py:615-645) */
 
 #define FM_FP32 0 /* physics state and arithmetic in float  (north-star configuration) */
 #define FM_FP64 1 /* physics state and arithmetic in double (bit-for-bit twin of the oracle's precision) */

@@ -10,19 +10,27 @@ qpos / qvel; integer task state, RNG, scores, num_obj and done flags compared bi
 import numpy as np
 
 
-def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights=(0.2, 0.4, 0.1, 0.4)):
+def random_actions(rng, env_class, act_dim, amp=2.0):
+    """one env-step of random actions for the class: toggles MultiDiscrete {0, 1}, FactoryManipulationEnv none"""
+    if env_class in ("PauseIKToggleEnv", "BackupIKToggleEnv"):
+        return rng.integers(0, 2, act_dim).astype(np.float32)
+    return rng.uniform(-amp, amp, act_dim).astype(np.float32)
+
+
+def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights=(0.2, 0.4, 0.1, 0.4),
+            env_class="AllFullRLProgressRewardEnv"):
     """oracle rollout from reset: state records before each step, actions, post-step results.
     Episodes that terminate are reset (SB3 auto-reset), so T may span several episodes."""
     from factory_marl_amd import state as st
 
     rng = np.random.default_rng(seed_actions)
-    e = oracle.Env(A, K, 42, reward=reward, weights=weights)
+    e = oracle.Env(A, K, 42, weights=weights, env_class=env_class)
     e.reset()
     recs, acts, outs = [], [], []
     for t in range(T):
         d, i, r = e.export_state()
         recs.append(st.pack(A, K, d, i, r))
-        a = rng.uniform(-amp, amp, 8 * A).astype(np.float32)
+        a = random_actions(rng, env_class, e.act_dim, amp)
         obs, rew, term, _, info = e.step(a)
         d2, i2, r2 = e.export_state()
         outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
@@ -65,7 +73,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     obs, rew, term = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
     tobs = env.terminal_obs.cpu().numpy()
     nq = 1 + 7 * K + 9 * A
-    errs, err_steps, int_bad, flag_bad, obs_err, rew_err = [], [], [], [], [], []
+    errs, err_steps, int_bad, flag_bad, obs_err, rew_err, ik_err = [], [], [], [], [], [], []
     for s in range(n):
         o = outs[s]
         if bool(term[s]) != o["term"]:
@@ -75,8 +83,11 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
             obs_err.append(np.abs(tobs[s] - o["obs"]).max())
             continue
         gd, gi, gr = st.unpack(A, K, got[s])
-        if not (np.array_equal(gi[:2 * K + 10], o["ints"][:2 * K + 10]) and np.array_equal(gr, o["rng"])):
+        if not (np.array_equal(gi[:2 * K + 10], o["ints"][:2 * K + 10]) and np.array_equal(gr, o["rng"])
+                and np.array_equal(gi[2 * K + 11:], o["ints"][2 * K + 11:])):  # + the IK policies' FSM block
             int_bad.append(s)
+        nd_base = len(gd) - 27 * A
+        ik_err.append(float(np.abs(gd[nd_base:] - o["dbl"][nd_base:]).max()) if A else 0.0)
         qd, vd = state_err(A, K, gd, o["dbl"])
         errs.append(max(qd.max(), vd.max()))
         err_steps.append(s)
@@ -89,7 +100,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     cnt = env.counters()
     env.close()
     return dict(errs=np.array(errs), err_steps=np.array(err_steps, int), int_bad=int_bad, flag_bad=flag_bad,
-                obs_err=np.array(obs_err), rew_err=np.array(rew_err), counters=cnt,
+                obs_err=np.array(obs_err), rew_err=np.array(rew_err), counters=cnt, ik_err=np.array(ik_err),
                 terms=int(sum(o["term"] for o in outs)), max_cubes=max(o["info"]["num_obj"] for o in outs))
 
 
