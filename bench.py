@@ -133,6 +133,48 @@ def timed_run(ctx, args, precision, steps, warmup, lo, hi):
     return wall, kern_ms, dc
 
 
+def timed_run_ppo(ctx, args, lo, hi):
+    """config 3: PPO rollout with the PyTorch-ROCm policy ([128, 128] tanh MLPs, SB3 MlpPolicy) in the loop --
+    policy forward, Gaussian sampling, clip, env-step, rollout-buffer writes are all inside the timed region;
+    then one PPO update (GAE + n_epochs x minibatches) over the collected rollout, timed separately"""
+    import torch
+
+    from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.ppo import PPO
+
+    A, K, N = args.arms, args.objects, hi - lo
+    env = FactoryVecEnv(N, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42), device=ctx.local_rank,
+                        precision=args.precision, seeds=arena_seeds(lo, hi, args.seeds))
+    env.reset()
+    preroll(env, args.preroll, ctx.rank, ctx.device)
+    dist = None
+    if ctx.world > 1:
+        import torch.distributed as dist
+    ppo = PPO(env, n_steps=args.steps, batch_size=args.ppo_batch, n_epochs=args.ppo_epochs, seed=ctx.rank, dist=dist)
+    ppo._last_obs = env.obs.clone()
+    ppo._last_starts = torch.zeros(N, device=ctx.device)
+    ppo.hp["n_steps"] = args.warmup
+    if args.warmup:
+        ppo.collect_rollouts()
+    ppo.hp["n_steps"] = args.steps
+    torch.cuda.synchronize()
+    c0 = env.counters()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    buf, _ = ppo.collect_rollouts()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = time.perf_counter() - t0
+    dc = env.counters() - c0
+    t1 = time.perf_counter()
+    ppo.train(buf)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    train_s = time.perf_counter() - t1
+    env.close()
+    return wall, train_s, dc
+
+
 def diagnostics(dc, N, steps, frame_skip=100):
     es = N * steps
     return {"env_steps_timed": es,
@@ -172,7 +214,13 @@ def main():
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "pmc_valu.json"),
                     help="VALU instruction counts per arena env-step by rocprofv3 --pmc (tools/pmc_valu.py)")
+    ap.add_argument("--workload", default="config2", choices=["config2", "config3"],
+                    help="config2: the headline (random policy); config3: 16384 arenas 2x8 PPO rollout")
+    ap.add_argument("--ppo-batch", type=int, default=16384)
+    ap.add_argument("--ppo-epochs", type=int, default=10)
     args = ap.parse_args()
+    if args.workload == "config3":
+        return main_config3(args)
 
     ctx = RankContext.from_env()
     A, K, N = args.arms, args.objects, args.arenas
@@ -237,6 +285,46 @@ def main():
             line["fp64_value"] = fp64
         if ctx.world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(A, K, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def main_config3(args):
+    """BASELINE config 3: 16384 arenas, 2 arms x 8 objects, PPO rollout with the PyTorch-ROCm policy, 1 MI355X
+    (per GPU with --gpus N: weak scaling, gradient / advantage all-reduce in the PPO update only)"""
+    if args.arenas == 4096:
+        args.arenas = 16384
+    if args.objects == 4:
+        args.objects = 8
+    if args.steps == 100:
+        args.steps = 16
+    if args.warmup == 10:
+        args.warmup = 2
+    ctx = RankContext.from_env()
+    A, K, N = args.arms, args.objects, args.arenas
+    lo, hi = rank_arenas(N, ctx.world, ctx.rank, "weak")
+    wall, train_s, dc = timed_run_ppo(ctx, args, lo, hi)
+    wall = ctx.max_over_ranks(wall)
+    train_s = ctx.max_over_ranks(train_s)
+    value = job_throughput(N, args.steps, ctx.world, wall)
+    if ctx.rank == 0:
+        line = {
+            "metric": "env-steps/sec (whole node), 16384 arenas 2-arm×8-obj PPO rollout; MI355X",
+            "value": round(value, 2), "unit": "env-steps/s", "n_gpus": ctx.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f64",
+            "data": "synthetic: PPO rollout of a freshly initialised MlpPolicy [128, 128] (SB3 init), Gaussian "
+                    f"sampling; scene seed 42; {args.preroll}-step desynchronising pre-roll",
+            "config": {"workload": f"config 3: {N} arenas/GPU, {A} arms x {K} objects, AllFullRLProgressRewardEnv, "
+                                   "PPO rollout (policy forward + sampling + env-step + buffer writes timed)",
+                       "arenas_per_gpu": N, "num_arms": A, "max_num_objects": K,
+                       "parallelism": f"arena-sharded x{ctx.world}; RCCL all-reduce in the update only"},
+            "ppo_update": {"seconds": round(train_s, 4), "samples": N * args.steps * ctx.world,
+                           "samples_per_s": round(N * args.steps * ctx.world / train_s, 1),
+                           "n_epochs": args.ppo_epochs, "batch_size_per_rank": args.ppo_batch},
+            "iteration_env_steps_per_s": round(N * args.steps * ctx.world / (wall + train_s), 2),
+            "diagnostics": diagnostics(dc, N, args.steps),
+        }
         print(json.dumps(line), flush=True)
     ctx.close()
 
