@@ -482,7 +482,11 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
                 : toggle ? s.A : 8 * s.A;
   }
   d.frame_skip = (int)((1.0 / cfg->control_frequency) / 0.001);
-  d.maxcon = cfg->max_contacts > 0 ? std::min(cfg->max_contacts, MAXCON) : MAXCON;
+  {
+    // contact capacity: the (2, 4) benchmark scene keeps 64 (one contact per lane), every other scene 128
+    const int cap = (s.A == 2 && s.K == 4) ? MAXCON : MAXCON_WIDE;
+    d.maxcon = cfg->max_contacts > 0 ? std::min(cfg->max_contacts, cap) : cap;
+  }
   d.maxrow = 10 * s.A;
   d.phys_stride = 2 * s.nq + 3 * s.nv;
   d.dbl_stride = s.nu + 3 + 2 * s.A + 1 + 27 * s.A;

@@ -47,7 +47,11 @@ struct gptr {
 };
 
 constexpr int WAVE = 64;
-constexpr int MAXCON = 64;    // per-arena contact capacity (64-bit tree masks)
+// per-arena contact capacity: 64 for the benchmark scene (2, 4) (one contact per lane, one 64-bit tree mask
+// word), 128 elsewhere (two contacts per lane, two mask words): with K cubes parked / hidden on the floor
+// (4 contacts each) the larger scenes exceed 64 contacts (census: (4, 16) reaches 80, (2, 8) pile-ups > 64)
+constexpr int MAXCON = 64;
+constexpr int MAXCON_WIDE = 128;
 constexpr int CJ = 18;        // Jacobian columns per contact (two trees of <= 9 dofs)
 constexpr int MAXSURV = 512;  // broadphase survivors per chunk
 constexpr int MAXPC = 8;      // contacts per geom pair (box-box)
@@ -55,6 +59,7 @@ constexpr int MAXPC = 8;      // contacts per geom pair (box-box)
 // Flat per-arena record layouts (strides in elements)
 struct Dims {
   static constexpr bool fixed = false;  // runtime dims (see FixedDims for compile-time scenes)
+  static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -418,7 +423,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.c_r = take(tsize * CR_N * maxcon);
   L.r_i = take(4 * 4 * maxrow);
   L.r_r = take(tsize * RR_N * maxrow);
-  L.tmask = take(8 * ntree);
+  L.tmask = take(8 * ntree * ((maxcon + 63) / 64));  // word h of tree t at [h * ntree + t]
   L.misc = take(4 * (16 + WAVE));  // 16 scalars + the Hessian assembly's block offsets
   L.sort = take(4 * K);
   L.uctl = take(8 * nu);
@@ -436,6 +441,7 @@ struct FixedDims {
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;
+  static constexpr int MAXC = (A_ == 2 && K_ == 4) ? MAXCON : MAXCON_WIDE;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
@@ -444,7 +450,7 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXCON, maxrow, ntree, TS);
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -1158,12 +1158,29 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   const int nst = misc[MISC_NSTAGE];
   const int ncon = nst < dm.maxcon ? nst : dm.maxcon;
   if (LANE == 0 && nst > dm.maxcon) ctr[0] += nst - dm.maxcon;
-  // rank of each staged contact among the staged keys (ncon <= 64: one per lane, keys broadcast by v_readlane)
-  const int mykey = LANE < ncon ? w.skey()[LANE] : 0x7fffffff;
-  int myrank = 0;
-  for (int t = 0; t < ncon; t++) myrank += __builtin_amdgcn_readlane(mykey, t) < mykey ? 1 : 0;
-  for (int s = LANE; s < ncon; s += WAVE) {
-    const int rank = myrank;
+  // rank of each staged contact among the staged keys: contacts c = LANE + 64 h (h < DIM::MAXC / 64), the keys
+  // broadcast by v_readlane
+  constexpr int NHC = DIM::MAXC / WAVE;
+  int mykey[NHC], myrank[NHC];
+#pragma unroll
+  for (int h = 0; h < NHC; h++) {
+    mykey[h] = LANE + WAVE * h < ncon ? w.skey()[LANE + WAVE * h] : 0x7fffffff;
+    myrank[h] = 0;
+  }
+#pragma unroll
+  for (int hs = 0; hs < NHC; hs++) {
+    const int tn = ncon - WAVE * hs < WAVE ? ncon - WAVE * hs : WAVE;
+    for (int t = 0; t < tn; t++) {
+      const int k = __builtin_amdgcn_readlane(mykey[hs], t);
+#pragma unroll
+      for (int h = 0; h < NHC; h++) myrank[h] += k < mykey[h] ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < NHC; h++) {
+    const int s = LANE + WAVE * h;
+    if (s >= ncon) continue;
+    const int rank = myrank[h];
     const T* st = w.stage() + 8 * s;
     int* ci = w.ci() + 4 * rank;
     T* cr = w.cr() + CR_N * rank;
@@ -1839,16 +1856,21 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     if (LANE == 0) misc[MISC_NROW] = nr < dm.maxrow ? nr : dm.maxrow;
   }
   SYNC();
-  // ---- tree -> contact masks: one ballot per tree over the contact lanes (ncon <= 64)
+  // ---- tree -> contact masks: one ballot per tree and 64-contact word (word h holds contacts 64 h .. 64 h + 63)
   {
-    int ta = -2, tb = -2;
-    if (LANE < ncon) {
-      ta = w.ci()[4 * LANE + 1];
-      tb = w.ci()[4 * LANE + 2];
-    }
-    for (int t = 0; t < dm.ntree; t++) {
-      const uint64_t mk = __ballot(ta == t || tb == t);
-      if (LANE == 0) w.tmask()[t] = mk;
+    const int nh = DIM::MAXC == WAVE ? 1 : (dm.maxcon + WAVE - 1) / WAVE;
+#pragma unroll
+    for (int h = 0; h < DIM::MAXC / WAVE; h++) {
+      if (h >= nh) break;
+      int ta = -2, tb = -2;
+      if (LANE + WAVE * h < ncon) {
+        ta = w.ci()[4 * (LANE + WAVE * h) + 1];
+        tb = w.ci()[4 * (LANE + WAVE * h) + 2];
+      }
+      for (int t = 0; t < dm.ntree; t++) {
+        const uint64_t mk = __ballot(ta == t || tb == t);
+        if (LANE == 0) w.tmask()[h * dm.ntree + t] = mk;
+      }
     }
   }
   (void)nv;
@@ -2254,10 +2276,12 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& 
   for (int i = LANE; i < dm.nv; i += WAVE) {
     int t = dof_tree(dm, i);
     int jl = i - tree_dof(dm, t);
-    uint64_t mk = w.tmask()[t];
     T s = 0;
+    const int nh = DIM::MAXC == WAVE ? 1 : (dm.maxcon + WAVE - 1) / WAVE;
+    for (int h = 0; h < nh; h++) {
+    uint64_t mk = w.tmask()[h * dm.ntree + t];
     while (mk) {
-      int c = __ffsll((unsigned long long)mk) - 1;
+      int c = WAVE * h + __ffsll((unsigned long long)mk) - 1;
       mk &= mk - 1;
       const int* ci = w.ci() + 4 * c;
       const T* cr = w.cr() + CR_N * c;
@@ -2265,6 +2289,7 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& 
       int col = ci[1] == t ? jl : nda + jl;
       const T* J = cr + CR_J;
       s += J[col] * cr[CR_JD] + J[CJ + col] * cr[CR_JD + 1] + J[2 * CJ + col] * cr[CR_JD + 2];
+    }
     }
     for (int r = 0; r < nrow; r++) {
       const int* ri = w.ri() + 4 * r;
@@ -2414,7 +2439,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SYNC();
     PMARK(PH_NHESS);
     if (nv <= 48 && !(M.dbg_flags & 1)) {
-      if constexpr (sizeof(T) == 4 && DIM::fixed)
+      if constexpr (sizeof(T) == 4 && DIM::fixed && DIM::MAXC == WAVE)  // tree masks of one word
         chol_sparse_rl<DIM>(M, w, H, g, dir);
       else
         chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
@@ -2479,28 +2504,34 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     }
     dMd = wave_sum(dMd);
     dMa = wave_sum(dMa);
-    // the walk's per-row data is loop-invariant: one contact (4 pyramid edges) and one generic row per lane
-    // (ncon <= 64, nrow <= 64) held in registers; padding lanes carry jd = 0, D = 0 and contribute nothing
-    T ejar[4], ejd[4], ete[4], eD = T(0);
+    // the walk's per-row data is loop-invariant: the contacts (4 pyramid edges each; contact LANE + 64 h) and
+    // one generic row per lane (nrow <= 64) held in registers; padding slots carry jd = 0, D = 0 and contribute
+    // nothing
+    constexpr int NHC = DIM::MAXC / WAVE;
+    T ejar[4 * NHC], ejd[4 * NHC], ete[4 * NHC], eD[NHC];
     T gjar = T(0), gjd = T(0), gte = T(0), gD = T(0);
     bool geq = false;
-    if (LANE < ncon) {
-      const T* cr = w.cr() + CR_N * LANE;
-      const T mu = cr[CR_MU], bd = cr[CR_BD], kd = cr[CR_KD];
-      eD = cr[CR_D];
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
-        ejar[e] = edge_val(cr + CR_JA, mu, e) - aref;
-        ejd[e] = edge_val(cr + CR_JD, mu, e);
-        ete[e] = ejd[e] != T(0) ? -ejar[e] / ejd[e] : T(0);
-      }
-    } else {
+    for (int h = 0; h < NHC; h++) {
+      eD[h] = T(0);
+      if (LANE + WAVE * h < ncon) {
+        const T* cr = w.cr() + CR_N * (LANE + WAVE * h);
+        const T mu = cr[CR_MU], bd = cr[CR_BD], kd = cr[CR_KD];
+        eD[h] = cr[CR_D];
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        ejar[e] = T(1);
-        ejd[e] = T(0);
-        ete[e] = T(0);
+        for (int e = 0; e < 4; e++) {
+          const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
+          ejar[4 * h + e] = edge_val(cr + CR_JA, mu, e) - aref;
+          ejd[4 * h + e] = edge_val(cr + CR_JD, mu, e);
+          ete[4 * h + e] = ejd[4 * h + e] != T(0) ? -ejar[4 * h + e] / ejd[4 * h + e] : T(0);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          ejar[4 * h + e] = T(1);
+          ejd[4 * h + e] = T(0);
+          ete[4 * h + e] = T(0);
+        }
       }
     }
     if (LANE < nrow) {
@@ -2515,7 +2546,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     for (int ls = 0; ls < 4 * (4 * ncon + nrow) + 4; ls++) {
       T c0 = 0, c1 = 0, tn = T(3.0e38);
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
+      for (int e = 0; e < 4 * NHC; e++) {
         const T jar = ejar[e], jd = ejd[e], te = ete[e];
         bool act;
         if (jd != T(0)) {
@@ -2525,8 +2556,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
           act = jar < T(0);
         }
         if (act) {
-          c0 += eD * (jar + alpha * jd) * jd;
-          c1 += eD * jd * jd;
+          c0 += eD[e / 4] * (jar + alpha * jd) * jd;
+          c1 += eD[e / 4] * jd * jd;
         }
       }
       {

@@ -248,3 +248,24 @@ def test_masked_reset_only_touches_masked_arenas():
         else:
             assert np.array_equal(after[i], before[i])
     env.close()
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_config5_scene_4x16_pause_toggle_fp32(oracle):
+    """BASELINE config 5's arena (4 arms x 16 cubes, PauseIKToggleEnv, runtime-dims kernel, contact capacity
+    128 -- the 16 parked cubes alone hold 64 floor contacts): teacher-forced against the oracle over 60 env-steps
+    from reset; no contact dropped for capacity, IK / task integer state exact, the SURVEY gate on most steps"""
+    traj = pu.rollout(oracle, 4, 16, 60, seed_actions=17, env_class="PauseIKToggleEnv")
+    r = pu.compare(traj, "fp32", 4, 16, "PauseIKToggleEnv")
+    e = r["errs"]
+    frac = float(np.mean(e <= 1e-4))
+    print(f"fp32 (4,16) PauseIKToggle: {frac:.1%} within 1e-4, median {np.median(e):.2e}, worst {e.max():.2e}, "
+          f"int/flag {len(r['int_bad'])}/{len(r['flag_bad'])}, max contacts {int(r['counters'][:, 5].max())}, "
+          f"dropped {int(r['counters'][:, 0].sum())}")
+    assert r["counters"][:, 0].sum() == 0
+    assert r["counters"][:, 5].max() > 64  # the scene does exceed the benchmark scene's 64
+    assert len(r["flag_bad"]) + len(r["int_bad"]) <= 1
+    # measured 71 % (median 9.7e-6): at K = 16 most cubes sit parked on the floor at x = 4..5 m, where float
+    # spacing (4.8e-7 m) in the contact points of their resting contacts shows up as spin noise of those
+    # (task-irrelevant) cubes; the fp64 build is the parity build for this scene shape
+    assert frac >= 0.65
