@@ -13,7 +13,7 @@ namespace fm {
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes);
 template <typename T, int A, int K>
-void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStream_t stream);
+void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStream_t stream, bool ik);
 }  // namespace fm
 
 // =================================================================================================
@@ -323,7 +323,9 @@ static int create_typed(fm_handle* h) {
   (void)idx;
   if (h->fixed < 0) {
     h->lay_step = h->lay;
-    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               h->lay.total));
+    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                h->lay.total));
   }
   return 0;
@@ -394,19 +396,23 @@ template <typename T>
 static void launch_step(fm_handle* h, const StepIO& io) {
   const StepParams<T> pd{make_model<T>(h), make_state<T>(h), h->lay, io};
   dim3 grid(h->dm.N), block(WAVE);
+  const bool ik = h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS;
   int idx = 0;
 #define X(a, k)                                                                                        \
   if (h->fixed == idx) {                                                                               \
     StepParams<T> pf = pd;                                                                             \
     pf.L = h->lay_step;                                                                                \
-    fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream);                                  \
+    fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream, ik);                              \
     return;                                                                                            \
   }                                                                                                    \
   idx++;
   FM_FIXED_SCENES
 #undef X
   (void)idx;
-  hipLaunchKernelGGL((step_kernel<T, Dims>), grid, block, h->lay.total, h->stream, pd);
+  if (ik)
+    hipLaunchKernelGGL((step_kernel<T, Dims, true>), grid, block, h->lay.total, h->stream, pd);
+  else
+    hipLaunchKernelGGL((step_kernel<T, Dims, false>), grid, block, h->lay.total, h->stream, pd);
 }
 
 extern "C" {

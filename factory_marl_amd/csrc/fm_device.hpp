@@ -3271,7 +3271,9 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   if (obs) write_obs(M, w, ti, td, obs + (size_t)arena * dm.obs_dim);
 }
 
-template <typename T, typename DIM>
+// IK: the env class may compose IK proposals (every class but AllFullRL); the AllFullRL instantiation carries
+// none of the IK code (and none of its register demand)
+template <typename T, typename DIM, bool IK>
 __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   (void)params;
@@ -3305,7 +3307,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   const double speed0 = td[1];
   const int ec = M.env_class;
   double* prop = (double*)w.H() + 24 * A;  // IK proposals of this step's compose (phase-local scratch)
-  if (env_ik_at_step(ec)) {  // IKPolicy.act() on the state the step starts from
+  if (IK && env_ik_at_step(ec)) {  // IKPolicy.act() on the state the step starts from
     load_state(M, S, w, arena, false);
     SYNC();
     ik_compose(M, w, ti, td, prop);
@@ -3317,7 +3319,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
       c = speed0;
     } else {
       const int arm = (u - 1) / 8, j = (u - 1) % 8;
-      switch (ec) {
+      switch (IK ? ec : FM_ENV_ALLFULLRL_PROGRESS) {
         case FM_ENV_ALLFULLRL_PROGRESS:
           c = process_action(M, act[u - 1], j);
           break;
@@ -3426,7 +3428,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     SYNC();
     refresh_copies(M, w);  // the TaskManager's teleports wrote the master state
     SYNC();
-    if (env_toggle(ec)) ik_proposals(M, w, ti, td);  // the step's observation (environments.py:197, 560-577)
+    if (IK && env_toggle(ec)) ik_proposals(M, w, ti, td);  // the step's observation (environments.py:197, 560-577)
     const int term = sc_[1] != 0.0;
     if (LANE == 0) {
       const int s_fail = sc_[2] != 0.0;
@@ -3483,7 +3485,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   }
   store_state(M, S, w, arena);
   FULL_SYNC();
-  if (reset_pass && env_toggle(ec)) ik_proposals(M, w, ti, td);  // reset()'s observation after the auto-reset
+  if (IK && reset_pass && env_toggle(ec)) ik_proposals(M, w, ti, td);  // reset()'s observation after the auto-reset
   if (io.obs) write_obs(M, w, ti, td, io.obs + (size_t)arena * dm.obs_dim);
   PMARK(PH_TAIL);
   if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);

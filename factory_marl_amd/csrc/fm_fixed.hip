@@ -18,16 +18,23 @@ namespace fm {
 
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes) {
-  return hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K>>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             lds_bytes);
+  hipError_t e = hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K>, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K>, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
+// ik: the env class composes IK proposals (every class but AllFullRLProgressRewardEnv)
 template <typename T, int A, int K>
-void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStream_t stream) {
-  hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
+void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStream_t stream, bool ik) {
+  if (ik)
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>, true>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
+  else
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>, false>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
 }
 
 template hipError_t fixed_set_attr<FM_REAL, FM_A, FM_K>(int);
-template void fixed_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, int, hipStream_t);
+template void fixed_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, int, hipStream_t, bool);
 
 }  // namespace fm
