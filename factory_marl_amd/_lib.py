@@ -63,7 +63,7 @@ class FmInfo(C.Structure):
 EXPORTED = [
     "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
-    "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile",
+    "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile", "fm_scene_mjcf",
 ]
 
 _LIB = None
@@ -111,6 +111,8 @@ def load():
     L.fm_debug_dump.restype = I
     L.fm_profile.argtypes = [P, I, P]
     L.fm_profile.restype = I
+    L.fm_scene_mjcf.argtypes = [I, I, C.c_uint64, C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.fm_scene_mjcf.restype = I
     _LIB = L
     return L
 
@@ -118,3 +120,14 @@ def load():
 def check(rc):
     if rc != 0:
         raise FactorySimError(f"factorysim error {rc}: {load().fm_last_error().decode()}")
+
+
+def scene_mjcf(num_arms=2, max_num_objects=10, seed=42, meshdir=None):
+    """The compiled scene as an MJCF string (include/factorysim.h fm_scene_mjcf; scene.py:109-161)."""
+    L = load()
+    n = C.c_size_t(0)
+    md = meshdir.encode() if meshdir else None
+    check(L.fm_scene_mjcf(num_arms, max_num_objects, seed, md, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value + 1)
+    check(L.fm_scene_mjcf(num_arms, max_num_objects, seed, md, buf, n.value + 1, C.byref(n)))
+    return buf.value.decode()

@@ -685,4 +685,18 @@ int fm_get_counters(fm_handle* h, int64_t* host_out) {
   return FM_OK;
 }
 
+// host only (no device): the compiled scene as MJCF (scene.py:109-161), for the MuJoCo cross-check
+int fm_scene_mjcf(int num_arms, int max_num_objects, uint64_t seed, const char* meshdir, char* buf, size_t cap,
+                  size_t* len) {
+  SceneHost s;
+  std::string err;
+  if (!build_scene(num_arms, max_num_objects, 1, &seed, s, err)) return set_err(FM_EINVAL, err);
+  const std::string x = export_mjcf(s, seed, meshdir);
+  if (len) *len = x.size();
+  if (!buf) return FM_OK;
+  if (cap < x.size() + 1) return set_err(FM_EINVAL, "buffer too small for the MJCF document (see *len)");
+  std::memcpy(buf, x.c_str(), x.size() + 1);
+  return FM_OK;
+}
+
 }  // extern "C"

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <tuple>
@@ -681,6 +682,322 @@ bool build_scene(int A, int K, int N, const uint64_t* seeds, SceneHost& s, std::
   for (int j = 0; j < s.nv; j++)
     for (int i = j; i < s.nv; i++) s.tri.push_back((uint32_t)i | ((uint32_t)j << 16));
   return true;
+}
+
+}  // namespace fm
+
+// ------------------------------------------------------------------------------------------------
+// MJCF export: the scene this compiler builds, as one flat MJCF document that
+// MuJoCo loads without dm_control, for the optional MuJoCo cross-check.  The element tree follows
+// dm_control's attach semantics of build_scene (scene.py:109-161): every attached model becomes an
+// attachment-frame body named "<model>/", element names carry the namescope prefixes base_env.py and
+// ik_policy.py look up (base_env.py:114-126, ik_policy.py:41-45), and unnamed geoms get dm_control's
+// "<scope>//unnamed_geom_<j>" names -- so body, joint, geom and actuator ids are those of the
+// reference's compiled model.  Kinematics, inertias, contact parameters and ranges are written from
+// the SceneHost tables the kernel runs on (angles as quaternions; limits spelled out, since the flat
+// document has no per-file compiler settings).  Visual meshes (iiwa14.xml, contype 0) are written as
+// mesh geoms when a mesh directory is given and otherwise as non-colliding 1 mm spheres in the same
+// slots, which keeps the geom numbering without the mesh files.
+// ------------------------------------------------------------------------------------------------
+namespace fm {
+
+namespace {
+
+void mat2quat(const double R[9], double q[4]) {
+  const double tr = R[0] + R[4] + R[8];
+  if (tr > 0) {
+    double s = 0.5 / std::sqrt(tr + 1.0);
+    q[0] = 0.25 / s;
+    q[1] = (R[7] - R[5]) * s;
+    q[2] = (R[2] - R[6]) * s;
+    q[3] = (R[3] - R[1]) * s;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    double s = 2.0 * std::sqrt(1.0 + R[0] - R[4] - R[8]);
+    q[0] = (R[7] - R[5]) / s;
+    q[1] = 0.25 * s;
+    q[2] = (R[1] + R[3]) / s;
+    q[3] = (R[2] + R[6]) / s;
+  } else if (R[4] > R[8]) {
+    double s = 2.0 * std::sqrt(1.0 + R[4] - R[0] - R[8]);
+    q[0] = (R[2] - R[6]) / s;
+    q[1] = (R[1] + R[3]) / s;
+    q[2] = 0.25 * s;
+    q[3] = (R[5] + R[7]) / s;
+  } else {
+    double s = 2.0 * std::sqrt(1.0 + R[8] - R[0] - R[4]);
+    q[0] = (R[3] - R[1]) / s;
+    q[1] = (R[2] + R[6]) / s;
+    q[2] = (R[5] + R[7]) / s;
+    q[3] = 0.25 * s;
+  }
+  if (q[0] < 0)
+    for (int k = 0; k < 4; k++) q[k] = -q[k];
+}
+
+std::string num(double x) {
+  char b[40];
+  std::snprintf(b, sizeof b, "%.17g", x == 0.0 ? 0.0 : x);
+  return b;
+}
+std::string vec(const double* v, int n) {
+  std::string s;
+  for (int i = 0; i < n; i++) s += (i ? " " : "") + num(v[i]);
+  return s;
+}
+
+struct Doc {
+  std::string out;
+  int depth = 0;
+  void open(const std::string& tag_attrs) {
+    out += std::string(2 * depth, ' ') + "<" + tag_attrs + ">\n";
+    depth++;
+  }
+  void close(const char* tag) {
+    depth--;
+    out += std::string(2 * depth, ' ') + "</" + tag + ">\n";
+  }
+  void leaf(const std::string& tag_attrs) { out += std::string(2 * depth, ' ') + "<" + tag_attrs + "/>\n"; }
+};
+
+// contact attributes of a parameter class (kPClass; priority 1 classes carry solref/solimp)
+std::string contact_attrs(int pc) {
+  const PClass& p = kPClass[pc];
+  if (pc == 0) return "";
+  return " solref=\"" + vec(p.solref, 2) + "\" solimp=\"" + vec(p.solimp, 5) + "\" priority=\"" +
+         std::to_string(p.priority) + "\"";
+}
+
+// iiwa14.xml visual meshes per body (base, link1..7) in XML order, with their material
+struct Vis {
+  int body;
+  const char* mesh;
+  const char* material;
+};
+const Vis kVis[] = {{0, "link_0", "gray"},         {1, "link_1", "gray"},        {2, "link_2_orange", "orange"},
+                    {2, "link_2_grey", "gray"},    {3, "link_3", "gray"},        {3, "band", "light_gray"},
+                    {3, "kuka", "black"},          {4, "link_4_orange", "orange"}, {4, "link_4_grey", "gray"},
+                    {5, "link_5", "gray"},         {5, "band", "light_gray"},    {5, "kuka", "black"},
+                    {6, "link_6_orange", "orange"}, {6, "link_6_grey", "gray"},  {7, "link_7", "gray"}};
+
+}  // namespace
+
+std::string export_mjcf(const SceneHost& s, uint64_t seed, const char* meshdir) {
+  const int A = s.A, K = s.K;
+  const bool mesh = meshdir && meshdir[0];
+  Doc d;
+  d.open("mujoco model=\"factory_scene_A" + std::to_string(A) + "_K" + std::to_string(K) + "_seed" +
+         std::to_string((unsigned long long)seed) + "\"");
+  d.leaf(std::string("compiler angle=\"radian\" autolimits=\"true\"") +
+         (mesh ? " meshdir=\"" + std::string(meshdir) + "\"" : ""));
+  // scene.xml:2 integrator / timestep; MuJoCo's defaults for the rest, spelled out (the kernel's solver)
+  d.leaf("option timestep=\"0.001\" integrator=\"implicitfast\" cone=\"pyramidal\" solver=\"Newton\" "
+         "iterations=\"100\" tolerance=\"1e-08\" ls_iterations=\"50\"");
+  d.open("visual");
+  d.leaf("headlight diffuse=\"0.6 0.6 0.6\" ambient=\"0.3 0.3 0.3\" specular=\"0 0 0\"");
+  d.leaf("rgba haze=\"0.15 0.25 0.35 1\"");
+  d.leaf("global azimuth=\"120\" elevation=\"-20\"");
+  d.close("visual");
+  d.leaf("statistic center=\"0 0 0\" extent=\"3\"");
+  d.open("asset");
+  d.leaf("texture type=\"skybox\" builtin=\"gradient\" rgb1=\"0.3 0.5 0.7\" rgb2=\"0 0 0\" width=\"512\" height=\"3072\"");
+  d.leaf("texture type=\"2d\" name=\"groundplane\" builtin=\"checker\" mark=\"edge\" rgb1=\"0.2 0.3 0.4\" "
+         "rgb2=\"0.1 0.2 0.3\" markrgb=\"0.8 0.8 0.8\" width=\"300\" height=\"300\"");
+  d.leaf("material name=\"groundplane\" texture=\"groundplane\" texuniform=\"true\" texrepeat=\"5 5\" "
+         "reflectance=\"0.2\"");
+  d.leaf("material name=\"iiwa14/gray\" specular=\"0.5\" shininess=\"0.25\" rgba=\"0.4 0.4 0.4 1\"");
+  d.leaf("material name=\"iiwa14/light_gray\" specular=\"0.5\" shininess=\"0.25\" rgba=\"0.6 0.6 0.6 1\"");
+  d.leaf("material name=\"iiwa14/black\" specular=\"0.5\" shininess=\"0.25\" rgba=\"0 0 0 1\"");
+  d.leaf("material name=\"iiwa14/orange\" specular=\"0.5\" shininess=\"0.25\" rgba=\"1 0.423529 0.0392157 1\"");
+  if (mesh) {
+    const char* meshes[] = {"link_0", "link_1", "link_2_orange", "link_2_grey", "link_3",  "band",
+                            "kuka",   "link_4_orange", "link_4_grey", "link_5", "link_6_orange", "link_6_grey",
+                            "link_7"};
+    for (const char* m : meshes) d.leaf(std::string("mesh name=\"iiwa14/") + m + "\" file=\"" + m + ".obj\"");
+  }
+  d.close("asset");
+
+  d.open("worldbody");
+  d.leaf("light pos=\"0 0 1.5\" dir=\"0 0 -1\" directional=\"true\"");
+  d.leaf("geom name=\"floor\" type=\"plane\" size=\"0 0 0.05\" material=\"groundplane\"");
+  const GeomRec& tg = s.geoms[1];
+  d.open("body name=\"table/\"");
+  d.leaf("geom name=\"table/table\" type=\"box\" pos=\"" + vec(tg.pos, 3) + "\" size=\"" + vec(tg.size, 3) + "\"" +
+         contact_attrs(1));
+  d.close("body");
+  // conveyor_belt.xml:4-12
+  d.open("body name=\"conveyor_belt/\"");
+  d.open("body name=\"conveyor_belt/conveyor\" pos=\"0 0 1.05\"");
+  d.leaf("joint name=\"conveyor_belt/conveyor_linear\" type=\"slide\" axis=\"0 1 0\" solreflimit=\"0.08 1\" "
+         "damping=\"0.0005\"");
+  d.leaf("geom name=\"conveyor_belt/belt\" type=\"box\" size=\"" + vec(s.geoms[2].size, 3) +
+         "\" mass=\"1000\" rgba=\"0.3 0.3 0.3 1\" friction=\"" + num(kPClass[2].fr) + " 0.01 0.01\"" +
+         contact_attrs(2));
+  d.close("body");
+  d.close("body");
+  // cubes (scene.py:121-133): the seed's draws -- size, then rgba[4] with alpha forced to 1
+  {
+    Pcg64 r = Pcg64::from_seed(seed);
+    for (int k = 0; k < K; k++) {
+      double h = 0.03 + (0.05 - 0.03) * r.next_double();
+      double rgba[4];
+      for (int c = 0; c < 4; c++) rgba[c] = r.next_double();
+      rgba[3] = 1.0;
+      const double sz[3] = {h, h, h};
+      std::string nm = "cube" + std::to_string(k) + "/";
+      d.open("body name=\"" + nm + "\"");
+      d.leaf("freejoint name=\"" + nm + "unnamed_joint_0\"");
+      d.leaf("geom name=\"" + nm + "cube\" type=\"box\" size=\"" + vec(sz, 3) + "\" mass=\"" +
+             num(1000.0 * std::pow(h, 3.0)) + "\" rgba=\"" + vec(rgba, 4) + "\" friction=\"1 0.01 0.01\"");
+      d.close("body");
+    }
+  }
+  // buckets (scene.py:64-106, 136-145)
+  for (int b = 0; b < 2; b++) {
+    std::string nm = std::string("bucket") + (b ? "_1" : "") + "/";
+    const double bp[3] = {s.bucket_x[b], s.bucket_y, 1.05};
+    const GeomRec& ta = s.geoms[3 + K + 5 * b];
+    d.open("body name=\"" + nm + "\"");
+    d.open("body name=\"" + nm + "bucket\" pos=\"" + vec(bp, 3) + "\"");
+    d.leaf("geom name=\"" + nm + "target_area\" type=\"box\" pos=\"0 0 -0.040000000000000001\" size=\"" +
+           vec(ta.size, 3) + "\" rgba=\"1 1 1 1\"" + contact_attrs(1));
+    for (int f = 0; f < 4; f++) {
+      const GeomRec& fg = s.geoms[4 + K + 5 * b + f];
+      double q[4];
+      mat2quat(fg.R, q);
+      std::string fn = nm + "bucket_fence" + (f ? "_" + std::to_string(f) : std::string()) + "/";
+      d.leaf("site name=\"" + nm + "fence_site" + std::to_string(f) + "\" quat=\"" + vec(q, 4) + "\"");
+      d.open("body name=\"" + fn + "\" quat=\"" + vec(q, 4) + "\"");
+      d.leaf("geom name=\"" + fn + "fence\" type=\"box\" pos=\"0.25 0 0\" size=\"" + vec(fg.size, 3) +
+             "\" rgba=\"0.2 0.2 0.2 1\"" + contact_attrs(1));
+      d.close("body");
+    }
+    d.close("body");
+    d.close("body");
+  }
+  // arms (scene.py:41-61, 147-161; iiwa14.xml; gripper.xml)
+  for (int i = 0; i < A; i++) {
+    const std::string an = "arm" + std::to_string(i) + "/", iw = an + "iiwa14/", gr = iw + "single_gripper/";
+    double q[4];
+    mat2quat(s.arm_base[i] + 3, q);
+    d.open("body name=\"" + an + "\"");
+    d.leaf("site name=\"" + an + "player_site\" pos=\"" + vec(s.arm_base[i], 3) + "\" quat=\"" + vec(q, 4) + "\"");
+    d.open("body name=\"" + iw + "\" pos=\"" + vec(s.arm_base[i], 3) + "\" quat=\"" + vec(q, 4) + "\"");
+    int gj = 0;  // iiwa14 unnamed-geom counter
+    auto geoms_of = [&](int link) {
+      for (const Vis& v : kVis) {
+        if (v.body != link) continue;
+        std::string g = "geom name=\"" + iw + "/unnamed_geom_" + std::to_string(gj++) + "\" ";
+        if (mesh)
+          g += std::string("type=\"mesh\" mesh=\"iiwa14/") + v.mesh + "\" material=\"iiwa14/" + v.material + "\"";
+        else
+          g += std::string("type=\"sphere\" size=\"0.001\" material=\"iiwa14/") + v.material + "\"";
+        d.leaf(g + " contype=\"0\" conaffinity=\"0\" group=\"2\"");
+      }
+      for (int sI = 0; sI < NSPH; sI++) {
+        const SphereDef& sd = kSpheres[sI];
+        if (sd.link != link) continue;
+        const double p[3] = {sd.x, sd.y, sd.z};
+        d.leaf("geom name=\"" + iw + "/unnamed_geom_" + std::to_string(gj++) + "\" type=\"sphere\" size=\"" +
+               num(sd.r) + "\" pos=\"" + vec(p, 3) + "\" group=\"3\"");
+      }
+    };
+    d.open("body name=\"" + iw + "base\"");
+    d.leaf("inertial mass=\"5\" pos=\"-0.10000000000000001 0 0.070000000000000007\" diaginertia=\"0.050000000000000003 "
+           "0.059999999999999998 0.029999999999999999\"");
+    geoms_of(0);
+    for (int b = 0; b < 7; b++) {
+      double bq[4], iq[4];
+      mat2quat(s.body_local[b] + 3, bq);
+      mat2quat(s.body_iR[b], iq);
+      d.open("body name=\"" + iw + "link" + std::to_string(b + 1) + "\" pos=\"" + vec(s.body_local[b], 3) +
+             "\" quat=\"" + vec(bq, 4) + "\"");
+      d.leaf("inertial mass=\"" + num(s.body_mass[b]) + "\" pos=\"" + vec(s.body_ipos[b], 3) + "\" quat=\"" +
+             vec(iq, 4) + "\" diaginertia=\"" + vec(s.body_I[b], 3) + "\"");
+      d.leaf("joint name=\"" + iw + "joint" + std::to_string(b + 1) + "\" type=\"hinge\" axis=\"0 0 1\" limited=\"true\" "
+             "range=\"" + vec(s.dof_range[b], 2) + "\"");
+      geoms_of(b + 1);
+    }
+    d.leaf("site name=\"" + iw + "attachment_site\" pos=\"" + vec(s.body_local[7], 3) + "\"");
+    // gripper.xml attached at attachment_site
+    d.open("body name=\"" + gr + "\" pos=\"" + vec(s.body_local[7], 3) + "\"");
+    d.open("body name=\"" + gr + "gripper_base\"");
+    d.leaf("inertial mass=\"" + num(s.body_mass[7]) + "\" pos=\"" + vec(s.body_ipos[7], 3) + "\" diaginertia=\"" +
+           vec(s.body_I[7], 3) + "\"");
+    int gg = 0;
+    const std::string gattr = " condim=\"3\" friction=\"" + num(kPClass[4].fr) + " 0.01 0.01\"" + contact_attrs(4);
+    d.leaf("geom name=\"" + gr + "/unnamed_geom_" + std::to_string(gg++) +
+           "\" type=\"box\" pos=\"0 0 0.014999999999999999\" size=\"0.070000000000000007 0.025000000000000001 "
+           "0.014999999999999999\"" + gattr);
+    for (int p = 0; p < 2; p++) {
+      double pq[4];
+      mat2quat(s.body_local[8 + p] + 3, pq);
+      const std::string pn = gr + (p ? "right_plate" : "left_plate");
+      d.open("body name=\"" + pn + "\" pos=\"" + vec(s.body_local[8 + p], 3) + "\" quat=\"" + vec(pq, 4) + "\"");
+      d.leaf("inertial mass=\"" + num(s.body_mass[8 + p]) + "\" pos=\"0 0 0\" diaginertia=\"" + vec(s.body_I[8 + p], 3) +
+             "\"");
+      const double gp[4][3] = {{0, -0.0075, -0.01}, {0, -0.0075, 0.01}, {0, 0.0075, -0.01}, {0, 0.0075, 0.01}};
+      for (int g = 0; g < 4; g++)
+        d.leaf("geom name=\"" + gr + "/unnamed_geom_" + std::to_string(gg++) + "\" type=\"box\" pos=\"" +
+               vec(gp[g], 3) + "\" size=\"0.0050000000000000001 0.0074999999999999997 0.01\"" + gattr);
+      d.leaf("joint name=\"" + pn + "_slide_joint\" type=\"slide\" axis=\"1 0 0\" limited=\"true\" range=\"" +
+             vec(s.dof_range[7 + p], 2) + "\"");
+      d.close("body");
+    }
+    d.leaf("site name=\"" + gr + "between_gripper_plates\" pos=\"" + vec(s.grip_site, 3) + "\"");
+    d.close("body");  // gripper_base
+    d.close("body");  // gripper frame
+    for (int b = 0; b < 7; b++) d.close("body");
+    d.close("body");  // base
+    d.close("body");  // iiwa14 frame
+    d.close("body");  // arm frame
+  }
+  d.close("worldbody");
+
+  // contact excludes (iiwa14.xml:143-151, gripper.xml:50-54)
+  d.open("contact");
+  for (int i = 0; i < A; i++) {
+    const std::string iw = "arm" + std::to_string(i) + "/iiwa14/", gr = iw + "single_gripper/";
+    const char* ex[7][2] = {{"base", "link1"}, {"base", "link2"}, {"base", "link3"}, {"link1", "link3"},
+                            {"link3", "link5"}, {"link4", "link7"}, {"link5", "link7"}};
+    for (auto& e : ex) d.leaf("exclude body1=\"" + iw + e[0] + "\" body2=\"" + iw + e[1] + "\"");
+    d.leaf("exclude body1=\"" + gr + "gripper_base\" body2=\"" + gr + "left_plate\"");
+    d.leaf("exclude body1=\"" + gr + "gripper_base\" body2=\"" + gr + "right_plate\"");
+    d.leaf("exclude body1=\"" + gr + "left_plate\" body2=\"" + gr + "right_plate\"");
+  }
+  d.close("contact");
+  d.open("equality");
+  for (int i = 0; i < A; i++) {
+    const std::string gr = "arm" + std::to_string(i) + "/iiwa14/single_gripper/";
+    d.leaf("joint joint1=\"" + gr + "left_plate_slide_joint\" joint2=\"" + gr +
+           "right_plate_slide_joint\" solref=\"0.002 1\" solimp=\"0.97999999999999998 0.99990000000000001 0.001\"");
+  }
+  d.close("equality");
+  d.open("tendon");
+  for (int i = 0; i < A; i++) {
+    const std::string gr = "arm" + std::to_string(i) + "/iiwa14/single_gripper/";
+    d.open("fixed name=\"" + gr + "split\"");
+    d.leaf("joint joint=\"" + gr + "left_plate_slide_joint\" coef=\"0.5\"");
+    d.leaf("joint joint=\"" + gr + "right_plate_slide_joint\" coef=\"0.5\"");
+    d.close("fixed");
+  }
+  d.close("tendon");
+  // actuators in the compiled order the kernel's ctrl vector follows: belt, then per arm 7 joints + gripper
+  d.open("actuator");
+  d.leaf("velocity name=\"conveyor_belt/slide\" joint=\"conveyor_belt/conveyor_linear\" kv=\"10000\" "
+         "ctrllimited=\"true\" ctrlrange=\"" + vec(s.ctrlrange[0], 2) + "\"");
+  for (int i = 0; i < A; i++) {
+    const std::string iw = "arm" + std::to_string(i) + "/iiwa14/", gr = iw + "single_gripper/";
+    for (int j = 0; j < 7; j++)
+      d.leaf("general name=\"" + iw + "actuator" + std::to_string(j + 1) + "\" joint=\"" + iw + "joint" +
+             std::to_string(j + 1) + "\" gaintype=\"fixed\" biastype=\"affine\" gainprm=\"2000\" "
+             "biasprm=\"0 -2000 -200\" ctrllimited=\"true\" ctrlrange=\"" + vec(s.ctrlrange[1 + 8 * i + j], 2) + "\"");
+    d.leaf("general name=\"" + gr + "gripper_linear_actuator\" tendon=\"" + gr + "split\" dyntype=\"none\" "
+           "biastype=\"affine\" forcelimited=\"true\" forcerange=\"-100 100\" ctrllimited=\"true\" ctrlrange=\"" +
+           vec(s.ctrlrange[8 + 8 * i], 2) + "\" gainprm=\"100 0 0\" biasprm=\"0 -100 -10\"");
+  }
+  d.close("actuator");
+  d.close("mujoco");
+  return d.out;
 }
 
 }  // namespace fm

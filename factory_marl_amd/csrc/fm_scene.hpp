@@ -93,4 +93,8 @@ struct Pcg64 {
 
 bool build_scene(int A, int K, int N, const uint64_t* seeds, SceneHost& out, std::string& err);
 
+// flat MJCF document of a built scene with the cubes of arena seed `seed` (scene.py:109-161 as
+// dm_control compiles it); meshdir = directory of the iiwa14 .obj meshes, or null/empty for placeholders
+std::string export_mjcf(const SceneHost& s, uint64_t seed, const char* meshdir);
+
 }  // namespace fm

@@ -23,6 +23,7 @@
  */
 #ifndef FACTORYSIM_H
 #define FACTORYSIM_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -151,6 +152,16 @@ int fm_profile(fm_handle* h, int mode, uint64_t* host_out);
  * state and dump internals as float64 into host_out (capacity `cap` doubles).  Returns the number of
  * doubles written (< 0 on error).  Layout in factory_marl_amd/csrc/fm_device.hpp (debug_kernel). */
 int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int cap);
+
+/* Scene export (host only, no device needed): the scene fm_create builds for (num_arms,
+ * max_num_objects) with the cubes of arena seed `seed`, as one flat MJCF document -- the model
+ * build_scene(num_objects, seed=seed, num_arms) (challenge_env/scene.py:109-161) compiles to under
+ * dm_control, with its element names (base_env.py:114-126, ik_policy.py:41-45) and id order, for an
+ * optional MuJoCo cross-check.  meshdir: directory of the iiwa14 .obj files (visual meshes), or
+ * NULL/"" for non-colliding placeholders in the same geom slots.  *len receives the document length;
+ * with buf == NULL only the length is returned; otherwise cap must be >= *len + 1 (NUL-terminated). */
+int fm_scene_mjcf(int num_arms, int max_num_objects, uint64_t seed, const char* meshdir, char* buf, size_t cap,
+                  size_t* len);
 
 #ifdef __cplusplus
 }
