@@ -64,6 +64,7 @@ EXPORTED = [
     "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
     "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile", "fm_scene_mjcf",
+    "fm_render", "fm_render_ngeom",
 ]
 
 _LIB = None
@@ -113,6 +114,10 @@ def load():
     L.fm_profile.restype = I
     L.fm_scene_mjcf.argtypes = [I, I, C.c_uint64, C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
     L.fm_scene_mjcf.restype = I
+    L.fm_render.argtypes = [P, C.POINTER(C.c_int32), I, I, I, C.POINTER(C.c_float), P, P]
+    L.fm_render.restype = I
+    L.fm_render_ngeom.argtypes = [P]
+    L.fm_render_ngeom.restype = I
     _LIB = L
     return L
 

@@ -2,6 +2,7 @@
 // C ABI declared in include/factorysim.h.  The runtime-dims kernels are instantiated here; the
 // compile-time scene kernels live in fm_fixed.hip objects (one per scene in FM_FIXED_SCENES).
 #include "fm_device.hpp"
+#include "fm_render.hpp"
 
 // scenes with a compile-time specialised env-step kernel: X(num_arms, max_num_objects); must match the
 // fm_fixed_<A>_<K>.o objects the Makefile links
@@ -72,6 +73,12 @@ struct fm_handle {
   uint64_t* rng = nullptr;
   int64_t* counters = nullptr;
   unsigned long long* prof = nullptr;
+  // rendering (fm_render): colour tables uploaded on first use, scratch grown on demand
+  float* render_rgb = nullptr;   // [ngc][4]
+  float* cube_rgba = nullptr;    // [N][K][4]
+  float* render_frames = nullptr;
+  int* render_arenas = nullptr;
+  size_t render_cap = 0;          // arenas the scratch holds
   bool prof_on = false;
   int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
   Lay lay_step{};  // workspace layout of the env-step kernel in use
@@ -415,6 +422,59 @@ static void launch_step(fm_handle* h, const StepIO& io) {
     hipLaunchKernelGGL((step_kernel<T, Dims, false>), grid, block, h->lay.total, h->stream, pd);
 }
 
+// base colour of each collidable geom (assets/scene.xml, scene.py, conveyor_belt.xml, iiwa14.xml materials;
+// MuJoCo's default geom rgba 0.5 where none is given); cubes take the seed's draws (cube_rgba)
+static std::vector<float> render_colours(const SceneHost& s) {
+  const int ngc = (int)s.geoms.size(), K = s.K;
+  std::vector<float> c(4 * (size_t)ngc, 0.5f);
+  for (int g = 0; g < ngc; g++) {
+    const GeomRec& G = s.geoms[g];
+    float r = 0.5f, gr = 0.5f, b = 0.5f;
+    if (G.mjid == 2) {
+      r = gr = b = 0.3f;  // belt
+    } else if (G.mjid >= 3 + K && G.mjid < 13 + K) {
+      const bool target = (G.mjid - 3 - K) % 5 == 0;
+      r = gr = b = target ? 1.0f : 0.2f;  // bucket target area / fences
+    } else if (G.mjid >= 13 + K && G.pclass == 0) {
+      int link = G.kbody == 0 ? 0 : (G.kbody - 2 - K) % 10 + 1;  // collision sphere of this iiwa link
+      if (link == 2 || link == 4 || link == 6) {
+        r = 1.0f;
+        gr = 0.423529f;
+        b = 0.0392157f;
+      } else {
+        r = gr = b = 0.4f;
+      }
+    }
+    c[4 * g] = r;
+    c[4 * g + 1] = gr;
+    c[4 * g + 2] = b;
+    c[4 * g + 3] = 1.0f;
+  }
+  return c;
+}
+
+template <typename T>
+static int render_typed(fm_handle* h, int count, int width, int height, const RenderParams& rp0, float* frames,
+                        uint8_t* rgb) {
+  const int ngc = h->dm.ngc;
+  RenderParams rp = rp0;
+  rp.frames = frames;
+  rp.rgb = rgb;
+  HIPCHK(hipFuncSetAttribute((const void*)render_frames_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             h->lay.total));
+  hipLaunchKernelGGL((render_frames_kernel<T, Dims>), dim3(count), dim3(WAVE), h->lay.total, h->stream,
+                     make_model<T>(h), make_state<T>(h), h->lay, rp);
+  HIPCHK(hipGetLastError());
+  if (rgb) {
+    const int lds = ngc * RF_N * (int)sizeof(float);
+    HIPCHK(hipFuncSetAttribute((const void*)render_pixels_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    dim3 grid(rp.tiles_x * ((height + RTILE - 1) / RTILE), count);
+    hipLaunchKernelGGL(render_pixels_kernel, grid, dim3(WAVE), lds, h->stream, rp, ngc);
+    HIPCHK(hipGetLastError());
+  }
+  return FM_OK;
+}
+
 extern "C" {
 
 void fm_config_default(fm_config* c) {
@@ -527,6 +587,8 @@ void fm_destroy(fm_handle* h) {
   (void)hipStreamSynchronize(h->stream);
   if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
   for (void* p : h->allocs) (void)hipFree(p);
+  for (void* p : {(void*)h->render_rgb, (void*)h->cube_rgba, (void*)h->render_frames, (void*)h->render_arenas})
+    if (p) (void)hipFree(p);
   if (h->handoff) (void)hipEventDestroy(h->handoff);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);  // never a stream the caller handed in
   delete h;
@@ -683,6 +745,72 @@ int fm_get_counters(fm_handle* h, int64_t* host_out) {
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * FM_NCTR * sizeof(int64_t), hipMemcpyDeviceToHost));
   return FM_OK;
+}
+
+int fm_render_ngeom(const fm_handle* h) { return h ? h->dm.ngc : -1; }
+
+int fm_render(fm_handle* h, const int32_t* arenas, int count, int width, int height, const float* camera,
+              uint8_t* rgb, float* geom_frames) {
+  if (!h || !arenas) return set_err(FM_EINVAL, "null argument");
+  if (count < 0 || (count > 0 && (width < 1 || height < 1 || width > 8192 || height > 8192)))
+    return set_err(FM_EINVAL, "bad image size");
+  if (!rgb && !geom_frames) return set_err(FM_EINVAL, "nothing to write (rgb and geom_frames are both NULL)");
+  if ((size_t)h->dm.ngc * RF_N * sizeof(float) > 160 * 1024) return set_err(FM_EINVAL, "scene too large to render");
+  for (int i = 0; i < count; i++)
+    if (arenas[i] < 0 || arenas[i] >= h->dm.N) return set_err(FM_EINVAL, "arena index out of range");
+  if (count == 0) return FM_OK;
+  HIPCHK(hipSetDevice(h->device));
+  if (!h->render_rgb) {
+    std::vector<float> c = render_colours(h->sc);
+    HIPCHK(hipMalloc((void**)&h->render_rgb, c.size() * sizeof(float)));
+    HIPCHK(hipMemcpy(h->render_rgb, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc((void**)&h->cube_rgba, h->sc.cube_rgba.size() * sizeof(float)));
+    HIPCHK(hipMemcpy(h->cube_rgba, h->sc.cube_rgba.data(), h->sc.cube_rgba.size() * sizeof(float),
+                     hipMemcpyHostToDevice));
+  }
+  if ((size_t)count > h->render_cap) {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->render_frames) HIPCHK(hipFree(h->render_frames));
+    if (h->render_arenas) HIPCHK(hipFree(h->render_arenas));
+    h->render_frames = nullptr;
+    h->render_arenas = nullptr;
+    HIPCHK(hipMalloc((void**)&h->render_frames, (size_t)count * h->dm.ngc * RF_N * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&h->render_arenas, (size_t)count * sizeof(int)));
+    h->render_cap = count;
+  }
+  // the arena list is read by the kernel on the stream: a synchronous copy, ordered after queued work
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(h->render_arenas, arenas, (size_t)count * sizeof(int), hipMemcpyHostToDevice));
+  // MuJoCo free camera (mjv_cameraInModel): forward from azimuth / elevation, eye = lookat - distance * forward;
+  // default = the reference viewer's initial camera (scene.py:164-169), fovy 45 deg
+  const float def[6] = {-0.30914206f, -0.14805237f, 1.53675732f, 3.6720494f, 66.957422f, -28.843359f};
+  const float* c = camera ? camera : def;
+  const double az = c[4] * M_PI / 180.0, el = c[5] * M_PI / 180.0;
+  const double fw[3] = {std::cos(el) * std::cos(az), std::cos(el) * std::sin(az), std::sin(el)};
+  double rt[3] = {fw[1], -fw[0], 0.0};  // forward x z
+  const double rn = std::sqrt(rt[0] * rt[0] + rt[1] * rt[1]);
+  if (rn < 1e-9) return set_err(FM_EINVAL, "camera looks straight up or down");
+  rt[0] /= rn;
+  rt[1] /= rn;
+  const double up[3] = {rt[1] * fw[2] - rt[2] * fw[1], rt[2] * fw[0] - rt[0] * fw[2], rt[0] * fw[1] - rt[1] * fw[0]};
+  RenderParams rp{};
+  for (int k = 0; k < 3; k++) {
+    rp.eye[k] = (float)(c[k] - c[3] * fw[k]);
+    rp.fwd[k] = (float)fw[k];
+    rp.right[k] = (float)rt[k];
+    rp.up[k] = (float)up[k];
+  }
+  rp.tan_y = (float)std::tan(0.5 * 45.0 * M_PI / 180.0);
+  rp.aspect = (float)width / (float)height;
+  rp.width = width;
+  rp.height = height;
+  rp.tiles_x = (width + RTILE - 1) / RTILE;
+  rp.arenas = h->render_arenas;
+  rp.geom_rgb = h->render_rgb;
+  rp.cube_rgba = h->cube_rgba;
+  float* frames = geom_frames ? geom_frames : h->render_frames;
+  return h->fp64 ? render_typed<double>(h, count, width, height, rp, frames, rgb)
+                 : render_typed<float>(h, count, width, height, rp, frames, rgb);
 }
 
 // host only (no device): the compiled scene as MJCF (scene.py:109-161), for the MuJoCo cross-check

@@ -654,6 +654,7 @@ bool build_scene(int A, int K, int N, const uint64_t* seeds, SceneHost& s, std::
 
   // ---- per-arena cubes (scene.py:121-131: draws size, rgba[4] per cube) and constants
   s.cube.assign((size_t)N * K * 4, 0.0);
+  s.cube_rgba.assign((size_t)N * K * 4, 0.0f);
   s.meaninertia.assign(N, 0.0);
   s.rng_init.assign((size_t)N * 4, 0);
   for (int n = 0; n < N; n++) {
@@ -662,7 +663,9 @@ bool build_scene(int A, int K, int N, const uint64_t* seeds, SceneHost& s, std::
     double tr = 1000.0 + A * s.arm_trace_M;
     for (int k = 0; k < K; k++) {
       double h = 0.03 + (0.05 - 0.03) * r.next_double();
-      for (int c = 0; c < 4; c++) (void)r.next_double();
+      float* rgba = &s.cube_rgba[((size_t)n * K + k) * 4];
+      for (int c = 0; c < 4; c++) rgba[c] = (float)r.next_double();
+      rgba[3] = 1.0f;
       double m = 1000.0 * std::pow(h, 3.0);
       double I = m / 3.0 * (h * h + h * h);
       double* c = &s.cube[((size_t)n * K + k) * 4];

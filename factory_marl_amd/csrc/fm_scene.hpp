@@ -76,6 +76,7 @@ struct SceneHost {
   int ptab[5][5];                  // params index for (pclass g1, pclass g2)
   // per arena
   std::vector<double> cube;     // [N][K][4]: h, m, I, pad
+  std::vector<float> cube_rgba;  // [N][K][4]: the seed's colour draws (alpha 1), for rendering only
   std::vector<double> meaninertia;  // [N]
   std::vector<uint64_t> rng_init;   // [N][4]: PCG64 state hi, lo, inc hi, lo (TaskManager rng)
   std::vector<uint32_t> tri;        // column-major lower triangle (i | j << 16)

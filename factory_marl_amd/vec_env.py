@@ -248,6 +248,47 @@ class FactoryVecEnv:
             return [None] * int(mask.sum())
         raise AttributeError(method_name)
 
+    # ------------------------------------------------------------------ rendering (rendering.py, base_env.py:288)
+    def render_tensors(self, indices=None, width=480, height=480, camera=None, frames=False):
+        """Ray-cast the arenas `indices` (default: all) at their current state on the GPU (fm_render).
+
+        Returns a uint8 tensor [len(indices), height, width, 3] on the env's device (rgb_array layout) and,
+        with frames=True, the float [len(indices), ngeom, 20] geometry table it was cast from.  camera =
+        (lookat_x, lookat_y, lookat_z, distance, azimuth_deg, elevation_deg) or None for the reference
+        viewer's initial camera."""
+        torch = self.torch
+        self._bind_stream()
+        idx = np.ascontiguousarray(range(self.num_envs) if indices is None else indices, dtype=np.int32).reshape(-1)
+        img = torch.empty(len(idx), height, width, 3, dtype=torch.uint8, device=self.device)
+        fr = None
+        if frames:
+            fr = torch.empty(len(idx), self._L.fm_render_ngeom(self._h), 20, dtype=torch.float32, device=self.device)
+        cam = None if camera is None else (C.c_float * 6)(*[float(x) for x in camera])
+        _lib.check(self._L.fm_render(self._h, idx.ctypes.data_as(C.POINTER(C.c_int32)), len(idx), int(width),
+                                     int(height), cam, C.c_void_p(img.data_ptr()),
+                                     C.c_void_p(fr.data_ptr()) if fr is not None else None))
+        return (img, fr) if frames else img
+
+    def get_images(self, indices=None, width=480, height=480, camera=None):
+        """SB3 VecEnv.get_images: one rgb_array per env (numpy uint8 [H, W, 3])."""
+        img = self.render_tensors(indices, width, height, camera).cpu().numpy()
+        return list(img)
+
+    def render(self, mode="rgb_array", indices=None, width=480, height=480, camera=None):
+        """SB3 VecEnv.render("rgb_array"): the images of `indices` (default: up to the first 16 envs) tiled in a
+        grid, as SB3's tile_images does."""
+        if mode != "rgb_array":
+            raise NotImplementedError("only rgb_array rendering (the human viewer is out of scope)")
+        if indices is None:
+            indices = range(min(self.num_envs, 16))
+        imgs = np.stack(self.get_images(indices, width, height, camera))
+        n = len(imgs)
+        cols = int(np.ceil(np.sqrt(n)))
+        rows = int(np.ceil(n / cols))
+        pad = np.zeros((rows * cols - n,) + imgs.shape[1:], dtype=imgs.dtype)
+        grid = np.concatenate([imgs, pad]).reshape(rows, cols, height, width, 3)
+        return grid.transpose(0, 2, 1, 3, 4).reshape(rows * height, cols * width, 3)
+
     def seed(self, seed=None):
         # seeds are fixed at creation (build_scene + TaskManager use the same seed, base_env.py:300,53)
         return [None] * self.num_envs

@@ -153,6 +153,19 @@ int fm_profile(fm_handle* h, int mode, uint64_t* host_out);
  * doubles written (< 0 on error).  Layout in factory_marl_amd/csrc/fm_device.hpp (debug_kernel). */
 int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int cap);
 
+/* Offscreen rgb_array rendering (rendering.py:153-305 OffScreenViewer, 653-789 MujocoRenderer.render;
+ * base_env.py:288-306 render()), batched: `count` arenas (host int32 indices) at their current state are ray
+ * cast on the GPU into the device buffer rgb [count][height][width][3] uint8, row 0 = top (rgb_array layout).
+ * camera: host float[6] = lookat xyz, distance, azimuth, elevation (degrees; MuJoCo free-camera convention), or
+ * NULL for the reference viewer's initial camera (scene.py:164-169); fovy 45.  Drawn is the collision geometry
+ * the physics uses (arms as their collision spheres and gripper boxes).  geom_frames (optional device buffer,
+ * float [count][fm_render_ngeom][20]: MuJoCo geom id, type 0 plane / 1 sphere / 2 box, world pos[3], R[9]
+ * row-major, half sizes[3], rgb[3]) receives the geometry the image was cast from; rgb may be NULL to get only
+ * those.  Asynchronous on the handle's stream (the arena list is copied before the call returns). */
+int fm_render(fm_handle* h, const int32_t* arenas, int count, int width, int height, const float* camera,
+              uint8_t* rgb, float* geom_frames);
+int fm_render_ngeom(const fm_handle* h); /* collidable geoms per arena (rows of geom_frames) */
+
 /* Scene export (host only, no device needed): the scene fm_create builds for (num_arms,
  * max_num_objects) with the cubes of arena seed `seed`, as one flat MJCF document -- the model
  * build_scene(num_objects, seed=seed, num_arms) (challenge_env/scene.py:109-161) compiles to under
