@@ -2114,6 +2114,204 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<f
   SYNC();
 }
 
+// fp32, compile-time scene with 64 < nv <= 80 ((2,8), (2,10)): the same register Cholesky for the 64 leading
+// positions (lane j owns position j; cubes, then arms) with the remaining nv - 64 positions (the last arm dofs and
+// the belt) as a border:
+//  * the head pivots update the border rows of their own columns as usual (L[64+i][k] is lane k's entry, read
+//    with v_readlane from the pivot lane instead of from a row lane that does not exist);
+//  * the border's Schur complement S = H_BB - L_B L_B' (L_B = the border rows of L, 16 x 64 padded) is one
+//    16x16x64 product on the matrix cores: 16 chained v_mfma_f32_16x16x4_f32 whose A and B operands are the same
+//    LDS element per lane (A[i][k] = B[k][i] = L_B[i][k]);
+//  * S is factored densely on the first nv - 64 lanes; the solves run head forward, border forward (the border
+//    rows' sums over the head read from LDS), border backward, head backward.
+template <typename T, typename DIM>
+__device__ constexpr bool border_chol() {
+  if constexpr (sizeof(T) == 4 && DIM::fixed)
+    return DIM::nv > WAVE && DIM::nv <= WAVE + 16;
+  else
+    return false;
+}
+typedef float fm_f32x4 __attribute__((ext_vector_type(4)));
+template <typename DIM>
+__device__ __forceinline__ void chol_sparse_border(const Model<float>& M, const Ws<float, DIM>& w, float* H,
+                                                   const float* g, float* dir) {
+  constexpr int NV = DIM::nv, KK = DIM::K, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
+  constexpr int NH = WAVE, NB = NV - WAVE, NW = (DIM::MAXC + 63) / 64;
+  static_assert(NB > 0 && NB <= 16, "border of at most 16 positions");
+  const int j = LANE;
+  const int jo = j + 1;  // head positions are never the belt (position NV - 1)
+  auto dof_of = [](int p) { return p == NV - 1 ? 0 : p + 1; };
+  float col[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) col[i] = H[dof_of(i) * NV + jo];
+  float cs[NB];  // lanes j < NB: border column NH + j, rows NH .. NV - 1
+#pragma unroll
+  for (int i = 0; i < NB; i++) cs[i] = j < NB ? H[dof_of(NH + i) * NV + dof_of(NH + (j < NB ? j : 0))] : 0.0f;
+  // ---- tree coupling graph + fill-in (as chol_sparse_rl, tree masks of NW words)
+  unsigned adj[NT];
+  {
+    uint64_t tm[NW][NT];
+#pragma unroll
+    for (int h = 0; h < NW; h++)
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        const uint64_t m = w.tmask()[h * NT + t];
+        tm[h][t] = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
+      }
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      unsigned a = 0;
+#pragma unroll
+      for (int u = 0; u < NT; u++) {
+        uint64_t o = 0;
+#pragma unroll
+        for (int h = 0; h < NW; h++) o |= tm[h][t] & tm[h][u];
+        if (u != t && o) a |= 1u << u;
+      }
+      adj[t] = a;
+    }
+    auto rank = [](int t) { return t == 0 ? NT - 1 : t - 1; };
+#pragma unroll
+    for (int r = 0; r < NT; r++) {
+      const int t = r == NT - 1 ? 0 : r + 1;
+      unsigned later = 0;
+#pragma unroll
+      for (int u = 0; u < NT; u++)
+        if (rank(u) > r) later |= 1u << u;
+      const unsigned nb = adj[t] & later;
+#pragma unroll
+      for (int u = 0; u < NT; u++)
+        if (nb & (1u << u)) adj[u] |= nb & ~(1u << u);
+    }
+  }
+  SYNC();  // every lane has its columns: H is scratch from here on
+  // ---- head factor (coupled blocks only; border rows read from the pivot lane)
+  const float tiny = 1e-37f;
+  float dinv = 1.0f;
+  static_for<0, NH>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int tk = k < A0 - 1 ? 1 + k / 6 : 1 + KK + (k - (A0 - 1)) / 9;
+    float d = readlane(col[k], k);
+    d = d > tiny ? d : tiny;
+    const float ri = 1.0f / sqrtf(d);
+    const float lj = col[k] * ri;
+    if (j == k) dinv = ri;
+    if (j >= k) col[k] = lj;
+    const unsigned ak = adj[tk];
+    if (j > k) {
+      static_for<0, NT>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int ps = u == 0 ? NV - 1 : (u <= KK ? 6 * (u - 1) : A0 - 1 + 9 * (u - 1 - KK));
+        constexpr int pn = u == 0 ? 1 : (u <= KK ? 6 : 9);
+        if constexpr (ps + pn > k + 1) {
+          if (u == tk || (ak & (1u << u))) {
+            float lv[pn];
+#pragma unroll
+            for (int ii = 0; ii < pn; ii++) {
+              const int i = ps + ii;
+              lv[ii] = i <= k ? 0.0f : (i < NH ? readlane(lj, i < NH ? i : 0) : readlane(col[i], k) * ri);
+            }
+#pragma unroll
+            for (int ii = 0; ii < pn; ii++) {
+              const int i = ps + ii;
+              if (i > k) col[i] -= lv[ii] * lj;
+            }
+          }
+        }
+      });
+    }
+  });
+  // ---- border Schur complement on the matrix cores: S -= L_B L_B'
+  float* LB = H;              // [64 lanes][16]: L[NH + i][lane]
+  float* SC = H + 16 * WAVE;  // [16][16]
+#pragma unroll
+  for (int i = 0; i < 16; i++) LB[16 * j + i] = i < NB ? col[NH + (i < NB ? i : 0)] * dinv : 0.0f;
+  SYNC();
+  fm_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 16; s += 2) {  // two accumulators: the 40-cycle dependent latency overlaps
+    const float a0 = LB[16 * (4 * s + (j >> 4)) + (j & 15)];
+    const float a1 = LB[16 * (4 * (s + 1) + (j >> 4)) + (j & 15)];
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, a0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, a1, acc1, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) SC[16 * (4 * (j >> 4) + r) + (j & 15)] = acc0[r] + acc1[r];
+  SYNC();
+  if (j < NB) {
+#pragma unroll
+    for (int i = 0; i < NB; i++) cs[i] -= SC[16 * i + j];
+  }
+  // ---- dense factor of S on lanes j < NB
+  float dinvb = 1.0f;
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    float d = readlane(cs[k], k);
+    d = d > tiny ? d : tiny;
+    const float ri = 1.0f / sqrtf(d);
+    const float lj = cs[k] * ri;
+    if (j == k) dinvb = ri;
+    if (j >= k) cs[k] = lj;
+    if (j > k && j < NB) {
+      float lv[NB];
+#pragma unroll
+      for (int i = 0; i < NB; i++) lv[i] = i > k ? readlane(lj, i) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < NB; i++)
+        if (i > k) cs[i] -= lv[i] * lj;
+    }
+  }
+  // ---- forward: head, then the border rows (their sums over the head columns from LDS)
+  float acc = -g[jo];
+  float y = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NH; k++) {
+    const float yk = readlane(acc * dinv, k);
+    if (j == k) y = yk;
+    if (j > k) acc -= col[k] * yk;
+  }
+  float* ys = SC;  // SC was consumed into cs before the border factor
+  SYNC();
+  ys[j] = y;
+  SYNC();
+  float accb = 0.0f;
+  if (j < NB) {
+    float sum = 0.0f;
+#pragma unroll 16
+    for (int k = 0; k < NH; k++) sum += LB[16 * k + j] * ys[k];
+    accb = -g[dof_of(NH + j)] - sum;
+  }
+  float yb = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    const float yk = readlane(accb * dinvb, k);
+    if (j == k) yb = yk;
+    if (j > k && j < NB) accb -= cs[k] * yk;
+  }
+  // ---- backward: border, then the head (border columns folded in first)
+  float acc2b = yb, xb = 0.0f;
+#pragma unroll
+  for (int k = NB - 1; k >= 0; k--) {
+    const float xk = readlane(acc2b * dinvb, k);
+    if (j == k) xb = xk;
+    if (j < k) acc2b -= cs[k] * dinvb * xk;
+  }
+  float acc2 = y;
+#pragma unroll
+  for (int i = 0; i < NB; i++) acc2 -= col[NH + i] * dinv * readlane(xb, i);
+  float x = 0.0f;
+#pragma unroll
+  for (int k = NH - 1; k >= 0; k--) {
+    const float xk = readlane(acc2 * dinv, k);
+    if (j == k) x = xk;
+    if (j < k) acc2 -= col[k] * dinv * xk;
+  }
+  SYNC();
+  dir[jo] = x;
+  if (j < NB) dir[dof_of(NH + j)] = xb;
+  SYNC();
+}
+
 template <typename T, int NVM>
 __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const T* g, T* dir) {
   const int j = LANE;
@@ -2446,6 +2644,9 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       PMARK(PH_NCHOL);
     } else if (nv <= 64 && !(M.dbg_flags & 1)) {
       chol_solve_reg<T, 64>(H, w.bc(), nv, g, dir);
+      PMARK(PH_NCHOL);
+    } else if (border_chol<T, DIM>() && !(M.dbg_flags & 1)) {
+      if constexpr (border_chol<T, DIM>()) chol_sparse_border<DIM>(M, w, H, g, dir);
       PMARK(PH_NCHOL);
     } else {
       // dense Cholesky (right-looking over the column-major lower-triangle table)

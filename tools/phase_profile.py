@@ -17,13 +17,15 @@ def main():
     ap.add_argument("--arenas", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--arms", type=int, default=2)
+    ap.add_argument("--objects", type=int, default=4)
     ap.add_argument("--preroll", type=int, default=200, help="desynchronising pre-roll (bench.preroll)")
     args = ap.parse_args()
     import torch
 
     from factory_marl_amd import FactoryVecEnv
 
-    env = FactoryVecEnv(args.arenas, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42),
+    env = FactoryVecEnv(args.arenas, env_kwargs=dict(num_arms=args.arms, max_num_objects=args.objects, seed=42),
                         precision=args.precision)
     env.reset()
     import bench
@@ -50,6 +52,7 @@ def main():
     rep["_newton_iters_per_substep"] = round(float(c1[1] - c0[1]) / sub, 3)
     rep["_mean_objects_in_scene"] = round(float(c1[6] - c0[6]) / (args.arenas * args.steps), 3)
     rep["_preroll"] = args.preroll
+    rep["_scene"] = f"{args.arms}x{args.objects}"
     print(json.dumps(rep, indent=1))
 
 
