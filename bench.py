@@ -93,7 +93,14 @@ def preroll(env, steps, rank, device):
         m = (off == s).astype(np.uint8)
         if m.any():
             env.reset(mask=m)
-        env.step_tensors(torch.rand(N, env.act_dim, device=device, generator=g) * 2.0 - 1.0)
+        env.step_tensors(random_actions(env, torch.rand(N, env.act_dim, device=device, generator=g)))
+
+
+def random_actions(env, u):
+    """random policy of the env class: U[-1, 1] Box actions, or fair-coin MultiDiscrete toggles (0.0 / 1.0)"""
+    if env.env_class in ("PauseIKToggleEnv", "BackupIKToggleEnv"):
+        return (u < 0.5).float()
+    return u * 2.0 - 1.0
 
 
 def timed_run(ctx, args, precision, steps, warmup, lo, hi):
@@ -104,14 +111,14 @@ def timed_run(ctx, args, precision, steps, warmup, lo, hi):
     from factory_marl_amd import FactoryVecEnv
 
     A, K, N = args.arms, args.objects, hi - lo
-    env = FactoryVecEnv(N, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42), device=ctx.local_rank,
-                        precision=precision, seeds=arena_seeds(lo, hi, args.seeds))
+    env = FactoryVecEnv(N, env_class=args.env_class, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42),
+                        device=ctx.local_rank, precision=precision, seeds=arena_seeds(lo, hi, args.seeds))
     env.reset()
     preroll(env, args.preroll, ctx.rank, ctx.device)
     g = torch.Generator(device=ctx.device)
     g.manual_seed(0 + ctx.rank)
     total = warmup + steps
-    acts = torch.rand(total, N, env.act_dim, device=ctx.device, generator=g, dtype=torch.float32) * 2.0 - 1.0
+    acts = random_actions(env, torch.rand(total, N, env.act_dim, device=ctx.device, generator=g, dtype=torch.float32))
     for s in range(warmup):
         env.step_tensors(acts[s])
     torch.cuda.synchronize()
@@ -218,13 +225,17 @@ def main():
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "pmc_valu.json"),
                     help="VALU instruction counts per arena env-step by rocprofv3 --pmc (tools/pmc_valu.py)")
-    ap.add_argument("--workload", default="config2", choices=["config2", "config3"],
-                    help="config2: the headline (random policy); config3: 16384 arenas 2x8 PPO rollout")
+    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config5"],
+                    help="config2: the headline (random policy); config3: 16384 arenas 2x8 PPO rollout; config5: "
+                         "4 arms x 16 objects PauseIKToggleEnv, 4096 arenas per GPU (32768 on 8), random toggles")
     ap.add_argument("--ppo-batch", type=int, default=16384)
     ap.add_argument("--ppo-epochs", type=int, default=10)
     args = ap.parse_args()
+    args.env_class = "AllFullRLProgressRewardEnv"
     if args.workload == "config3":
         return main_config3(args)
+    if args.workload == "config5":
+        return main_config5(args)
 
     ctx = RankContext.from_env()
     A, K, N = args.arms, args.objects, args.arenas
@@ -289,6 +300,41 @@ def main():
             line["fp64_value"] = fp64
         if ctx.world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(A, K, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def main_config5(args):
+    """BASELINE config 5: 4 arms x 16 objects, PauseIKToggleEnv (IK base policy on every arm, MultiDiscrete toggles),
+    4096 arenas per GPU; random fair-coin toggles (the IK proposals drive the arms), auto-reset"""
+    args.arms, args.objects, args.env_class = 4, 16, "PauseIKToggleEnv"
+    if args.steps == 100:
+        args.steps = 20
+    if args.warmup == 10:
+        args.warmup = 2
+    if args.preroll == 200:
+        args.preroll = 100
+    ctx = RankContext.from_env()
+    A, K, N = args.arms, args.objects, args.arenas
+    lo, hi = rank_arenas(N, ctx.world, ctx.rank, "weak")
+    wall, kern_ms, dc = timed_run(ctx, args, args.precision, args.steps, args.warmup, lo, hi)
+    wall = ctx.max_over_ranks(wall)
+    value = job_throughput(N, args.steps, ctx.world, wall)
+    if ctx.rank == 0:
+        line = {
+            "metric": "env-steps/sec (whole node), 4096 arenas/GPU 4-arm x 16-obj PauseIKToggleEnv; MI355X",
+            "value": round(value, 2), "unit": "env-steps/s", "n_gpus": ctx.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f64",
+            "data": f"synthetic (fair-coin MultiDiscrete toggles, Philox seed 0+rank; scene seed 42; {args.preroll}-step "
+                    "desynchronising pre-roll)",
+            "config": {"workload": f"config 5: {N} arenas/GPU, {A} arms x {K} objects, PauseIKToggleEnv (float64 IK "
+                                   "base policy in the kernel), random toggles, 100 substeps/env-step, auto-reset",
+                       "arenas_per_gpu": N, "num_arms": A, "max_num_objects": K,
+                       "parallelism": f"arena-sharded x{ctx.world} (no collective)"},
+            "kernel_ms_avg": round(kern_ms, 4),
+            "diagnostics": diagnostics(dc, N, args.steps),
+        }
         print(json.dumps(line), flush=True)
     ctx.close()
 

@@ -2312,6 +2312,95 @@ __device__ __forceinline__ void chol_sparse_border(const Model<float>& M, const 
   SYNC();
 }
 
+// Sparse LDS Cholesky + solve for the scenes without a register path (runtime-dims scenes such as (4,16); fp64
+// above nv = 64): chol_sparse_rl's elimination order (cubes, arms, belt last) and tree-block sparsity with the
+// trailing matrix in LDS (lower triangle in elimination order, entry (i, c) at H[dof(i) * nv + dof(c)]).  Per
+// pivot the rows it touches -- later positions of its own tree and of the trees coupled to it, fill-in included --
+// are compacted by ballot; the column is scaled one row per lane, then one lane per column of that row set updates
+// its column.  The substitutions walk the same row sets.  Returns false (nothing written) when the scene has more
+// trees than a 32-bit coupling mask holds.
+template <typename T, typename DIM>
+__device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, DIM>& w, T* H, const T* g, T* dir) {
+  const DIM dm(M.dm);
+  const int NV = dm.nv, K = dm.K, NT = dm.ntree, A0 = 1 + 6 * K;
+  if (NT > 32) return false;
+  const int NW = (dm.maxcon + 63) / 64;
+  T* dinv = w.tmp();          // quad()'s scratch, dead until the line search
+  int* list = (int*)w.fa();   // actuator forces, consumed by smooth_acc
+  auto dof = [=](int p) { return p == NV - 1 ? 0 : p + 1; };
+  auto tree_of = [=](int p) { return p == NV - 1 ? 0 : (p < A0 - 1 ? 1 + p / 6 : 1 + K + (p - (A0 - 1)) / 9); };
+  // tree coupling graph (lane t: trees coupled to tree t), then the fill-in of the elimination order
+  unsigned adj = 0;
+  if (LANE < NT) {
+    for (int u = 0; u < NT; u++) {
+      uint64_t o = 0;
+      for (int h = 0; h < NW; h++) o |= w.tmask()[h * NT + LANE] & w.tmask()[h * NT + u];
+      if (u != LANE && o) adj |= 1u << u;
+    }
+  }
+  const unsigned all = NT < 32 ? (1u << NT) - 1u : ~0u;
+  for (int r = 0; r < NT; r++) {
+    const int t = r == NT - 1 ? 0 : r + 1;                                    // tree of rank r
+    unsigned later = (r + 2 < 32 ? (~0u << (r + 2)) : 0u) & all;            // trees u >= 1 of rank u - 1 > r
+    if (r < NT - 1) later |= 1u;                                             // the belt ranks last
+    const unsigned nb = (unsigned)__builtin_amdgcn_readlane((int)adj, t) & later;
+    if (LANE < NT && ((nb >> LANE) & 1u)) adj |= nb & ~(1u << LANE);
+  }
+  const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
+  for (int k = 0; k < NV; k++) {
+    const int tk = tree_of(k), dk = dof(k);
+    const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
+    T d = H[dk * NV + dk];
+    d = d > tiny ? d : tiny;
+    const T ri = T(1) / sqrt(d);
+    int m = 0;
+    for (int p0 = k + 1; p0 < NV; p0 += WAVE) {
+      const int p = p0 + LANE;
+      const bool in = p < NV && ((ak >> tree_of(p)) & 1u);
+      const uint64_t bal = __ballot(in);
+      const int below = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+      if (in) list[m + below] = p;
+      m += __popcll(bal);
+    }
+    if (LANE == 0) dinv[k] = ri;
+    SYNC();
+    for (int e = LANE; e < m; e += WAVE) H[dof(list[e]) * NV + dk] *= ri;  // L[i][k]
+    SYNC();
+    for (int b = LANE; b < m; b += WAVE) {
+      const int dc = dof(list[b]);
+      const T lc = H[dc * NV + dk];
+      for (int a = b; a < m; a++) {
+        const int di = dof(list[a]);
+        H[di * NV + dc] -= H[di * NV + dk] * lc;
+      }
+    }
+    SYNC();
+  }
+  for (int p = LANE; p < NV; p += WAVE) dir[dof(p)] = -g[dof(p)];
+  SYNC();
+  for (int k = 0; k < NV; k++) {  // L y = -g, column by column over the pivot's row set
+    const int tk = tree_of(k), dk = dof(k);
+    const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
+    const T yk = dir[dk] * dinv[k];
+    SYNC();
+    if (LANE == 0) dir[dk] = yk;
+    for (int p = k + 1 + LANE; p < NV; p += WAVE)
+      if ((ak >> tree_of(p)) & 1u) dir[dof(p)] -= H[dof(p) * NV + dk] * yk;
+    SYNC();
+  }
+  for (int k = NV - 1; k >= 0; k--) {  // L' x = y
+    const int tk = tree_of(k), dk = dof(k);
+    const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
+    const T xk = dir[dk] * dinv[k];
+    SYNC();
+    if (LANE == 0) dir[dk] = xk;
+    for (int p = LANE; p < k; p += WAVE)
+      if ((ak >> tree_of(p)) & 1u) dir[dof(p)] -= H[dk * NV + dof(p)] * xk;
+    SYNC();
+  }
+  return true;
+}
+
 template <typename T, int NVM>
 __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const T* g, T* dir) {
   const int j = LANE;
@@ -2647,6 +2736,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       PMARK(PH_NCHOL);
     } else if (border_chol<T, DIM>() && !(M.dbg_flags & 1)) {
       if constexpr (border_chol<T, DIM>()) chol_sparse_border<DIM>(M, w, H, g, dir);
+      PMARK(PH_NCHOL);
+    } else if (!(M.dbg_flags & 1) && chol_sparse_lds(M, w, H, g, dir)) {
       PMARK(PH_NCHOL);
     } else {
       // dense Cholesky (right-looking over the column-major lower-triangle table)
