@@ -2366,24 +2366,29 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
     SYNC();
     for (int e = LANE; e < m; e += WAVE) H[dof(list[e]) * NV + dk] *= ri;  // L[i][k]
     SYNC();
-    for (int b = LANE; b < m; b += WAVE) {
-      const int dc = dof(list[b]);
-      const T lc = H[dc * NV + dk];
-      for (int a = b; a < m; a++) {
-        const int di = dof(list[a]);
-        H[di * NV + dc] -= H[di * NV + dk] * lc;
-      }
+    // trailing update of the row set's lower triangle, one (row, column) pair per lane: the m (m + 1) / 2 pairs
+    // are spread over the wave (a pair's entry is written by that lane only; column dk is read-only here)
+    const int npair = m * (m + 1) / 2;
+    for (int e = LANE; e < npair; e += WAVE) {
+      int a = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);  // e -> (a >= b), packed lower triangle
+      if ((a + 1) * (a + 2) / 2 <= e) a++;
+      if (a * (a + 1) / 2 > e) a--;
+      const int b = e - a * (a + 1) / 2;
+      const int di = dof(list[a]), dc = dof(list[b]);
+      H[di * NV + dc] -= H[di * NV + dk] * H[dc * NV + dk];
     }
     SYNC();
   }
+  // substitutions: the forward pass reads dir as the running right-hand side and writes y to yv (the row list's
+  // array, free now), the backward pass runs on yv and writes x to dir -- one wave barrier per pivot
+  T* yv = (T*)w.fa();
   for (int p = LANE; p < NV; p += WAVE) dir[dof(p)] = -g[dof(p)];
   SYNC();
   for (int k = 0; k < NV; k++) {  // L y = -g, column by column over the pivot's row set
     const int tk = tree_of(k), dk = dof(k);
     const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
     const T yk = dir[dk] * dinv[k];
-    SYNC();
-    if (LANE == 0) dir[dk] = yk;
+    if (LANE == 0) yv[dk] = yk;
     for (int p = k + 1 + LANE; p < NV; p += WAVE)
       if ((ak >> tree_of(p)) & 1u) dir[dof(p)] -= H[dof(p) * NV + dk] * yk;
     SYNC();
@@ -2391,11 +2396,10 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
   for (int k = NV - 1; k >= 0; k--) {  // L' x = y
     const int tk = tree_of(k), dk = dof(k);
     const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
-    const T xk = dir[dk] * dinv[k];
-    SYNC();
+    const T xk = yv[dk] * dinv[k];
     if (LANE == 0) dir[dk] = xk;
     for (int p = LANE; p < k; p += WAVE)
-      if ((ak >> tree_of(p)) & 1u) dir[dof(p)] -= H[dk * NV + dof(p)] * xk;
+      if ((ak >> tree_of(p)) & 1u) yv[dof(p)] -= H[dk * NV + dof(p)] * xk;
     SYNC();
   }
   return true;
