@@ -2008,25 +2008,25 @@ __device__ __forceinline__ void contact_K(const Ws<T, DIM>& w, int ncon) {
 __device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
 
-// fp32, compile-time scene: Cholesky factor and solve of the Newton Hessian (assembled in LDS) for
+// compile-time scene (fp32 and fp64): Cholesky factor and solve of the Newton Hessian (assembled in LDS) for
 // dir = -H^-1 g, in registers (lane j owns column j; pivots and trailing operands broadcast by v_readlane).
 //  * Elimination order: cubes, arms, belt last (position p = dof - 1, the belt at NV - 1).  The belt touches
 //    every cube resting on it; eliminated last it is a border row instead of coupling all those cubes.
 //  * Tree-block sparsity: H couples two trees only through a contact between them.  The coupling graph (plus
 //    the fill-in of this elimination order) comes from the tree->contact masks; a pivot updates only the row
 //    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
-template <typename DIM>
-__device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<float, DIM>& w, const float* H,
-                                               const float* g, float* dir) {
+template <typename T, typename DIM>
+__device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const T* g,
+                                               T* dir) {
   constexpr int NV = DIM::nv, KK = DIM::K, AA = DIM::A, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
   const int j = LANE;
   const int jo = j == NV - 1 ? 0 : j + 1;  // lane j's dof (original numbering)
-  float col[NV];
+  T col[NV];
   // ---- H (assembled in LDS, row-major, original numbering) -> lane j holds column jo in elimination order
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     const int io = i == NV - 1 ? 0 : i + 1;
-    col[i] = j < NV ? H[io * NV + jo] : 0.0f;
+    col[i] = j < NV ? H[io * NV + jo] : T(0);
   }
   SYNC();
   // ---- tree coupling graph + fill-in of the elimination order (trees by rank: cubes, arms, belt)
@@ -2061,15 +2061,15 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<f
     }
   }
   // ---- factor (right-looking, pivots and trailing operands broadcast by v_readlane), coupled blocks only
-  const float tiny = 1e-37f;
-  float dinv = 1.0f;
+  const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
+  T dinv = T(1);
   static_for<0, NV>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int tk = k == NV - 1 ? 0 : (k < A0 - 1 ? 1 + k / 6 : 1 + KK + (k - (A0 - 1)) / 9);
-    float d = readlane(col[k], k);
+    T d = readlane(col[k], k);
     d = d > tiny ? d : tiny;
-    const float ri = 1.0f / sqrtf(d);
-    const float lj = col[k] * ri;
+    const T ri = T(1) / sqrt(d);
+    const T lj = col[k] * ri;
     if (j == k) dinv = ri;
     if (j >= k) col[k] = lj;
     const unsigned ak = adj[tk];
@@ -2082,9 +2082,9 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<f
           if (u == tk || (ak & (1u << u))) {             // coupled to the pivot's tree
             // the block's operands are broadcast first, then used: the v_readlane -> VALU hazard is paid once
             // per block instead of once per entry
-            float lv[pn];
+            T lv[pn];
 #pragma unroll
-            for (int ii = 0; ii < pn; ii++) lv[ii] = ps + ii > k ? readlane(lj, ps + ii) : 0.0f;
+            for (int ii = 0; ii < pn; ii++) lv[ii] = ps + ii > k ? readlane(lj, ps + ii) : T(0);
 #pragma unroll
             for (int ii = 0; ii < pn; ii++) {
               const int i = ps + ii;
@@ -2095,18 +2095,18 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<float>& M, const Ws<f
       });
     }
   });
-  float acc = j < NV ? -g[jo] : 0.0f;
-  float y = 0.0f;
+  T acc = j < NV ? -g[jo] : T(0);
+  T y = T(0);
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    const float yk = readlane(acc * dinv, k);
+    const T yk = readlane(acc * dinv, k);
     if (j == k) y = yk;
     if (j > k) acc -= col[k] * yk;
   }
-  float acc2 = y, x = 0.0f;
+  T acc2 = y, x = T(0);
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
-    const float xk = readlane(acc2 * dinv, k);
+    const T xk = readlane(acc2 * dinv, k);
     if (j == k) x = xk;
     if (j < k) acc2 -= col[k] * dinv * xk;
   }
@@ -2730,8 +2730,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SYNC();
     PMARK(PH_NHESS);
     if (nv <= 48 && !(M.dbg_flags & 1)) {
-      if constexpr (sizeof(T) == 4 && DIM::fixed && DIM::MAXC == WAVE)  // tree masks of one word
-        chol_sparse_rl<DIM>(M, w, H, g, dir);
+      if constexpr (DIM::fixed && DIM::MAXC == WAVE)  // tree masks of one word
+        chol_sparse_rl<T, DIM>(M, w, H, g, dir);
       else
         chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
       PMARK(PH_NCHOL);
