@@ -11,6 +11,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
+_LIB_F32 = None
 
 
 def build(force=False):
@@ -21,15 +22,28 @@ def build(force=False):
     return so
 
 
-def lib():
-    global _LIB
+def lib(f32=False):
+    """the oracle library; f32=True loads liboracle_f32.so, the same sources with every double a float (the fp32
+    floor study of tools/fp32_floor.py --float-oracle), whose real-valued arguments are float32"""
+    global _LIB, _LIB_F32
+    if f32:
+        if _LIB_F32 is None:
+            so = os.path.join(_HERE, "liboracle_f32.so")
+            subprocess.run(["make", "-s", "-C", _HERE, "liboracle_f32.so"], check=True)
+            _LIB_F32 = _bind(C.CDLL(so), C.c_float)
+        return _LIB_F32
     if _LIB is None:
         so = os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(so):
             build()
-        L = C.CDLL(so)
-        P, I, D, U64 = C.c_void_p, C.c_int, C.c_double, C.c_uint64
-        DP = C.POINTER(C.c_double)
+        _LIB = _bind(C.CDLL(so), C.c_double)
+    return _LIB
+
+
+def _bind(L, real):
+    if True:
+        P, I, D, U64 = C.c_void_p, C.c_int, real, C.c_uint64
+        DP = C.POINTER(real)
         sig = {
             "or_env_create": (P, [I, I, U64, I, DP]),
             "or_env_free": (None, [P]),
@@ -98,8 +112,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        _LIB = L
-    return _LIB
+    L.real = np.float32 if real is C.c_float else np.float64
+    L.c_real = real
+    return L
 
 
 def ptr(a):
@@ -115,8 +130,8 @@ CONTACT_BYTES = 8 * (1 + 3 + 9 + 1 + 2 + 5 + 1) + 4 * 4
 
 
 class Model:
-    def __init__(self, A, K, seed, handle=None):
-        L = lib()
+    def __init__(self, A, K, seed, handle=None, L=None):
+        L = self.L = L or lib()
         self.own = handle is None
         self.h = handle if handle is not None else L.or_model_create(A, K, seed)
         if not self.h:
@@ -126,62 +141,62 @@ class Model:
 
     def __del__(self):
         if getattr(self, "own", False) and self.h:
-            lib().or_model_free(self.h)
+            self.L.or_model_free(self.h)
 
     @property
     def cube_size(self):
-        return arr(lib().or_m_cube_size(self.h), self.K)
+        return arr(self.L.or_m_cube_size(self.h), self.K)
 
     @property
     def body_invweight0(self):
-        return arr(lib().or_m_body_invweight0(self.h), 2 * self.nbody).reshape(-1, 2)
+        return arr(self.L.or_m_body_invweight0(self.h), 2 * self.nbody).reshape(-1, 2)
 
     @property
     def dof_invweight0(self):
-        return arr(lib().or_m_dof_invweight0(self.h), self.nv)
+        return arr(self.L.or_m_dof_invweight0(self.h), self.nv)
 
     @property
     def meaninertia(self):
-        return lib().or_m_meaninertia(self.h)
+        return self.L.or_m_meaninertia(self.h)
 
     @property
     def ctrlrange(self):
-        return arr(lib().or_m_act_ctrlrange(self.h), 2 * self.nu).reshape(-1, 2)
+        return arr(self.L.or_m_act_ctrlrange(self.h), 2 * self.nu).reshape(-1, 2)
 
     @property
     def geom_body(self):
-        return arr(lib().or_m_geom_body(self.h), self.ngeom, np.int32)
+        return arr(self.L.or_m_geom_body(self.h), self.ngeom, np.int32)
 
     @property
     def geom_type(self):
-        return arr(lib().or_m_geom_type(self.h), self.ngeom, np.int32)
+        return arr(self.L.or_m_geom_type(self.h), self.ngeom, np.int32)
 
     @property
     def geom_size(self):
-        return arr(lib().or_m_geom_size(self.h), 3 * self.ngeom).reshape(-1, 3)
+        return arr(self.L.or_m_geom_size(self.h), 3 * self.ngeom).reshape(-1, 3)
 
     @property
     def body_mass(self):
-        return arr(lib().or_m_body_mass(self.h), self.nbody)
+        return arr(self.L.or_m_body_mass(self.h), self.nbody)
 
     def arm_geom_range(self, i):
-        L = lib()
+        L = self.L
         return L.or_m_arm_geom_lo(self.h)[i], L.or_m_arm_geom_hi(self.h)[i]
 
 
 class Data:
     def __init__(self, model, handle=None):
-        L = lib()
+        L = self.L = model.L
         self.m = model
         self.own = handle is None
         self.h = handle if handle is not None else L.or_data_create(model.h)
 
     def __del__(self):
         if getattr(self, "own", False) and self.h:
-            lib().or_data_free(self.h)
+            self.L.or_data_free(self.h)
 
     def _view(self, fn, n):
-        return np.ctypeslib.as_array(getattr(lib(), fn)(self.h), shape=(n,))
+        return np.ctypeslib.as_array(getattr(self.L, fn)(self.h), shape=(n,))
 
     @property
     def qpos(self):
@@ -241,46 +256,46 @@ class Data:
 
     @property
     def ncon(self):
-        return lib().or_d_ncon(self.h)
+        return self.L.or_d_ncon(self.h)
 
     @property
     def nefc(self):
-        return lib().or_d_nefc(self.h)
+        return self.L.or_d_nefc(self.h)
 
     @property
     def niter(self):
-        return lib().or_d_niter(self.h)
+        return self.L.or_d_niter(self.h)
 
     def contacts(self):
         out = []
         g = np.zeros(2, np.int32)
         v = np.zeros(14)
         for i in range(self.ncon):
-            lib().or_d_contact(self.h, i, ptr(g), ptr(v))
+            self.L.or_d_contact(self.h, i, ptr(g), ptr(v))
             out.append(dict(geom=tuple(int(x) for x in g), dist=v[0], pos=v[1:4].copy(),
                             frame=v[4:13].reshape(3, 3).copy(), mu=v[13]))
         return out
 
     def contact_force(self, i):
         f = np.zeros(6)
-        lib().or_contact_force(self.m.h, self.h, i, ptr(f))
+        self.L.or_contact_force(self.m.h, self.h, i, ptr(f))
         return f
 
     def step(self, ctrl=None):
-        c = np.zeros(self.m.nu) if ctrl is None else np.ascontiguousarray(ctrl, dtype=np.float64)
-        lib().or_physics_step(self.m.h, self.h, ptr(c))
+        c = np.zeros(self.m.nu, self.L.real) if ctrl is None else np.ascontiguousarray(ctrl, dtype=self.L.real)
+        self.L.or_physics_step(self.m.h, self.h, ptr(c))
 
     def forward(self):
-        lib().or_forward(self.m.h, self.h)
+        self.L.or_forward(self.m.h, self.h)
 
     def step1(self):
-        lib().or_step1(self.m.h, self.h)
+        self.L.or_step1(self.m.h, self.h)
 
     def jac(self, body, point):
         p = np.ascontiguousarray(point, dtype=np.float64)
         jp = np.zeros(3 * self.m.nv)
         jr = np.zeros(3 * self.m.nv)
-        lib().or_jac_point(self.m.h, self.h, body, ptr(p), ptr(jp), ptr(jr))
+        self.L.or_jac_point(self.m.h, self.h, body, ptr(p), ptr(jp), ptr(jr))
         return jp.reshape(3, -1), jr.reshape(3, -1)
 
 
@@ -295,16 +310,16 @@ class Env:
     """Oracle restatement of the env classes of src/environments.py (default AllFullRLProgressRewardEnv)."""
 
     def __init__(self, num_arms=2, max_num_objects=4, seed=42, reward="progress",
-                 weights=(0.2, 0.4, 0.0, 0.4), env_class=None):
-        L = lib()
-        w = (C.c_double * 4)(*weights)
+                 weights=(0.2, 0.4, 0.0, 0.4), env_class=None, f32=False):
+        L = self.L = lib(f32)
+        w = (L.c_real * 4)(*weights)
         if env_class is None:  # legacy selector: progress -> AllFullRL, score -> FactoryManipulationEnv
             env_class = "AllFullRLProgressRewardEnv" if reward == "progress" else "FactoryManipulationEnv"
         self.env_class = env_class
         self.h = L.or_env_create(num_arms, max_num_objects, seed, ENV_CLASSES[env_class], w)
         if not self.h:
             raise ValueError("bad env config")
-        self.model = Model(num_arms, max_num_objects, seed, handle=L.or_env_model(self.h))
+        self.model = Model(num_arms, max_num_objects, seed, handle=L.or_env_model(self.h), L=L)
         self.data = Data(self.model, handle=L.or_env_data(self.h))
         self.task = L.or_env_task(self.h)
         self.obs_dim = L.or_env_obs_dim(self.h)
@@ -312,37 +327,37 @@ class Env:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().or_env_free(self.h)
+            self.L.or_env_free(self.h)
             self.h = None
 
     def reset(self):
         obs = np.zeros(self.obs_dim, np.float32)
-        lib().or_env_reset(self.h, ptr(obs))
+        self.L.or_env_reset(self.h, ptr(obs))
         return obs
 
     def step(self, action):
         a = np.ascontiguousarray(action if self.act_dim else np.zeros(1), dtype=np.float32)
         obs = np.zeros(self.obs_dim, np.float32)
-        rew = C.c_double(0)
-        info = (C.c_double * 7)()
-        term = lib().or_env_step(self.h, ptr(a), ptr(obs), C.byref(rew), info)
+        rew = self.L.c_real(0)
+        info = (self.L.c_real * 7)()
+        term = self.L.or_env_step(self.h, ptr(a), ptr(obs), C.byref(rew), info)
         inf = dict(scores=[int(info[0]), int(info[1])], play_time=info[2], conveyor_speed=info[3],
                    out_of_reach=bool(info[4]), force_terminate=bool(info[5]), num_obj=int(info[6]))
         return obs, rew.value, bool(term), False, inf
 
     def task_int(self, what):
-        return lib().or_t_int(self.task, what.encode())
+        return self.L.or_t_int(self.task, what.encode())
 
     def task_double(self, what):
-        return lib().or_t_double(self.task, what.encode())
+        return self.L.or_t_double(self.task, what.encode())
 
     def in_scene(self):
         n = self.task_int("n_in")
-        p = lib().or_t_in_scene(self.task)
+        p = self.L.or_t_in_scene(self.task)
         return [p[i] for i in range(n)]
 
     def ctrl_target(self):
-        return arr(lib().or_t_ctrl_target(self.task), self.model.nu)
+        return arr(self.L.or_t_ctrl_target(self.task), self.model.nu)
 
     def state_sizes(self):
         m = self.model
@@ -354,24 +369,24 @@ class Env:
         """IKPolicy state of arm i: dict(state, counter, target, ignore, last_ctrl, move_start)"""
         ai = np.zeros(19, np.int32)
         ad = np.zeros(11)
-        lib().or_env_ik_arm(self.h, i, ptr(ai), ptr(ad))
+        self.L.or_env_ik_arm(self.h, i, ptr(ai), ptr(ad))
         return dict(state=int(ai[0]), counter=int(ai[1]), target=int(ai[2]), ignore=list(ai[3:3 + self.model.A]),
                     last_ctrl=ad[:8].copy(), move_start=ad[8:11].copy())
 
     def ik_steps(self):
-        return lib().or_env_ik_steps(self.h)
+        return self.L.or_env_ik_steps(self.h)
 
     def export_state(self):
         """full arena state in the product's record layout (fm_get_state)"""
         nd, ni = self.state_sizes()
-        dbl = np.zeros(nd)
+        dbl = np.zeros(nd, self.L.real)
         ints = np.zeros(ni, np.int32)
         rng = np.zeros(4, np.uint64)
-        lib().or_env_export(self.h, ptr(dbl), ptr(ints), ptr(rng))
+        self.L.or_env_export(self.h, ptr(dbl), ptr(ints), ptr(rng))
         return dbl, ints, rng
 
     def import_state(self, dbl, ints, rng):
-        dbl = np.ascontiguousarray(dbl, dtype=np.float64)
+        dbl = np.ascontiguousarray(dbl, dtype=self.L.real)
         ints = np.ascontiguousarray(ints, dtype=np.int32)
         rng = np.ascontiguousarray(rng, dtype=np.uint64)
-        lib().or_env_import(self.h, ptr(dbl), ptr(ints), ptr(rng))
+        self.L.or_env_import(self.h, ptr(dbl), ptr(ints), ptr(rng))

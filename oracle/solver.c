@@ -19,7 +19,9 @@
 #include "oracle.h"
 #include "oracle_internal.h"
 
-#define OR_SOLVER_TOL 1e-12
+#ifndef OR_SOLVER_TOL
+#define OR_SOLVER_TOL 1e-12 /* liboracle_f32.so (fp32 floor study) overrides it */
+#endif
 #define OR_SOLVER_ITER 100
 
 double or_impedance(const double si[5], double x) {

@@ -13,7 +13,13 @@ acceleration is multiplied by 1 + AMP*U(-1,1) (AMP = 2^-24 models ONE fp32 round
 substep, the least any fp32 physics incurs).  Steps that miss the gate under that perturbation are
 sensitive beyond fp32 resolution: their miss is inherent to fp32 arithmetic, not to a kernel.
 
-usage: python tools/fp32_floor.py [A K T seed_actions] [--accel-noise AMP] [--json out.json]
+Third probe (--float-oracle): the same algorithm in single precision -- liboracle_f32.so, the oracle's sources
+with every double a float (oracle/f32_prelude.h) -- teacher-forced from the float64 oracle's state rounded to
+float32, one env-step per trajectory step, against the float64 step.  This is the fp32 floor of the algorithm as
+written (a float state, float arithmetic throughout); the kernel's fp32 build keeps a float64 master state and a
+z-shifted frame on top of it, so its misses should be a subset of these.
+
+usage: python tools/fp32_floor.py [A K T seed_actions] [--accel-noise AMP | --float-oracle] [--json out.json]
 """
 import json
 import os
@@ -68,6 +74,30 @@ def floor_study(A, K, T, seed_actions=7, amp=1.0, rng_perturb=None, accel_noise=
     return out
 
 
+def float_oracle_study(A, K, T, seed_actions=7):
+    """per-step error of the float restatement stepped from the float64 oracle's state (rounded to float32)"""
+    rng = np.random.default_rng(seed_actions)
+    e = po.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4))
+    e.reset()
+    f = po.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4), f32=True)
+    f.reset()
+    out = []
+    for t in range(T):
+        d, i, r = e.export_state()
+        a = rng.uniform(-2, 2, 8 * A).astype(np.float32)
+        f.import_state(d.astype(np.float32), i, r)
+        _, _, term, _, info = e.step(a)
+        _, _, fterm, _, _ = f.step(a)
+        d2, i2, _ = e.export_state()
+        f2, fi2, _ = f.export_state()
+        flip = (term != fterm) or not np.array_equal(i2, fi2)
+        out.append(dict(step=t, err=None if term else rel_err(A, K, f2.astype(np.float64), d2), term=bool(term),
+                        flip=bool(flip), ncubes=int(info["num_obj"])))
+        if term:
+            e.reset()
+    return out
+
+
 def summarize(rows, gate=1e-4):
     e = np.array([r["err"] for r in rows if r["err"] is not None])
     return dict(steps=len(rows), compared=len(e), within=float(np.mean(e <= gate)), median=float(np.median(e)),
@@ -85,11 +115,12 @@ if __name__ == "__main__":
     if "--json" in argv:
         jpath = argv[argv.index("--json") + 1]
         del argv[argv.index("--json"):argv.index("--json") + 2]
+    fo = "--float-oracle" in argv
     args = [a for a in argv if not a.startswith("--")]
     A, K, T, sa = (int(x) for x in (args + ["2", "4", "96", "7"][len(args):]))
     po.build()
-    rows = floor_study(A, K, T, sa, accel_noise=noise)
+    rows = float_oracle_study(A, K, T, sa) if fo else floor_study(A, K, T, sa, accel_noise=noise)
     s = summarize(rows)
-    print(json.dumps(dict(A=A, K=K, T=T, seed_actions=sa, accel_noise=noise, **s)))
+    print(json.dumps(dict(A=A, K=K, T=T, seed_actions=sa, accel_noise=noise, float_oracle=fo, **s)))
     if jpath:
         json.dump(dict(summary=s, rows=rows), open(jpath, "w"), indent=1)
