@@ -75,7 +75,8 @@ def cpu_baseline(A, K, seconds):
     return {"value": round(n.value / dt, 3), "unit": "env-steps/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"{cores} arenas x {steps} env-steps ({A} arms x {K} objects, random actions), "
-                      f"oracle/ C restatement (fp64, dense Cholesky, OpenMP), {dt:.1f} s wall"}
+                      f"oracle/ C restatement (fp64, OpenMP; static collision-pair list with body-level bounds, "
+                      f"envelope Cholesky of M and the Newton Hessian, sparse constraint rows), {dt:.1f} s wall"}
 
 
 def preroll(env, steps, rank, device):

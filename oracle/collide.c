@@ -397,17 +397,67 @@ static void contact_param(const or_model* m, int g1, int g2, or_contact* c) {
   c->margin = m->geom_margin[g1] > m->geom_margin[g2] ? m->geom_margin[g1] : m->geom_margin[g2];
 }
 
+void or_collision_pairs(or_model* m) {
+  const size_t np = (size_t)(m->ngeom * (m->ngeom - 1) / 2 + 1);
+  free(m->cpair);
+  free(m->run_lo);
+  free(m->run_geom);
+  free(m->run_body);
+  free(m->run_margin);
+  m->ncpair = m->nrun = 0;
+  m->cpair = (int*)malloc(sizeof(int) * np);
+  m->run_lo = (int*)malloc(sizeof(int) * (np + 1));
+  m->run_geom = (int*)malloc(sizeof(int) * np);
+  m->run_body = (int*)malloc(sizeof(int) * np);
+  m->run_margin = (double*)malloc(sizeof(double) * np);
+  for (int ga = 0; ga < m->ngeom; ga++)
+    for (int gb = ga + 1; gb < m->ngeom; gb++) {
+      if (!pair_allowed(m, ga, gb)) continue;
+      const int bb = m->geom_body[gb];
+      const double mg = m->geom_margin[ga] > m->geom_margin[gb] ? m->geom_margin[ga] : m->geom_margin[gb];
+      if (m->nrun == 0 || m->run_geom[m->nrun - 1] != ga || m->run_body[m->nrun - 1] != bb) {
+        m->run_lo[m->nrun] = m->ncpair;
+        m->run_geom[m->nrun] = ga;
+        m->run_body[m->nrun] = bb;
+        m->run_margin[m->nrun++] = mg;
+      } else if (mg > m->run_margin[m->nrun - 1]) {
+        m->run_margin[m->nrun - 1] = mg;
+      }
+      int sw = m->geom_type[ga] > m->geom_type[gb];
+      m->cpair[m->ncpair++] = sw ? (gb | ga << 16) : (ga | gb << 16);
+    }
+  m->run_lo[m->nrun] = m->ncpair;
+}
+
+/* mj_collision over the static pair list.  CPU-baseline speed-up (not in the restated algorithm's results): a run
+ * of pairs (one geom against the geoms of one body) is skipped when the geom's bounding sphere misses the body's
+ * bounding sphere of its geoms' spheres -- then every pair of the run fails the per-pair rbound test below, which
+ * still decides each pair, so the contact list is the same, in the same order */
 void or_collision(const or_model* m, or_data* d) {
   d->ncon = 0;
   or_contact tmp[16];
-  for (int ga = 0; ga < m->ngeom; ga++) {
-    for (int gb = ga + 1; gb < m->ngeom; gb++) {
-      if (!pair_allowed(m, ga, gb)) continue;
-      int g1 = ga, g2 = gb;
-      if (m->geom_type[g1] > m->geom_type[g2]) {
-        g1 = gb;
-        g2 = ga;
-      }
+  double bc[3 * m->nbody], br[m->nbody];
+  for (int b = 0; b < m->nbody; b++) {
+    br[b] = 0;
+    for (int k = 0; k < 3; k++) bc[3 * b + k] = d->xpos[3 * b + k];
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    const int b = m->geom_body[g];
+    double v[3];
+    for (int k = 0; k < 3; k++) v[k] = d->geom_xpos[3 * g + k] - bc[3 * b + k];
+    const double r = m->geom_rbound[g] > 0 ? or_norm3(v) + m->geom_rbound[g] : INFINITY;
+    if (r > br[b]) br[b] = r;
+  }
+  for (int run = 0; run < m->nrun; run++) {
+    const int ga = m->run_geom[run], bb = m->run_body[run];
+    if (m->geom_rbound[ga] > 0 && br[bb] < INFINITY) {
+      double v[3];
+      for (int k = 0; k < 3; k++) v[k] = d->geom_xpos[3 * ga + k] - bc[3 * bb + k];
+      const double lim = m->geom_rbound[ga] + br[bb] + m->run_margin[run];
+      if (or_norm3(v) > lim * (1 + 1e-9) + 1e-9) continue;
+    }
+    for (int p = m->run_lo[run]; p < m->run_lo[run + 1]; p++) {
+      const int g1 = m->cpair[p] & 0xFFFF, g2 = m->cpair[p] >> 16;
       double margin = m->geom_margin[g1] > m->geom_margin[g2] ? m->geom_margin[g1] : m->geom_margin[g2];
       if (m->geom_rbound[g1] > 0 && m->geom_rbound[g2] > 0) {
         double v[3];

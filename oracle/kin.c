@@ -356,6 +356,44 @@ void or_chol_solve(const double* L, int n, double* x) {
   }
 }
 
+/* Envelope (profile) Cholesky, the CPU-baseline speed-up of or_cholesky: row i of L is zero left of f[i], the
+ * first nonzero of row i of A's lower triangle (fill-in stays inside the envelope), so every product skipped is
+ * an exact zero and the factor equals or_cholesky's bit for bit (up to the sign of zero entries).  M is block
+ * diagonal by kinematic tree and the Newton Hessian keeps tree-block sparsity (MuJoCo factors both sparsely). */
+void or_cholesky_env(double* A, int n, int* f) {
+  for (int i = 0; i < n; i++) {
+    int k = 0;
+    while (k < i && A[i * n + k] == 0) k++;
+    f[i] = k;
+  }
+  for (int j = 0; j < n; j++) {
+    double s = A[j * n + j];
+    for (int k = f[j]; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+    double ljj = sqrt(s > 1e-300 ? s : 1e-300);
+    A[j * n + j] = ljj;
+    for (int i = j + 1; i < n; i++) {
+      if (j < f[i]) continue; /* L[i][j] stays the exact zero of A */
+      double t = A[i * n + j];
+      for (int k = f[i] > f[j] ? f[i] : f[j]; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / ljj;
+    }
+  }
+}
+
+void or_chol_solve_env(const double* L, int n, const int* f, double* x) {
+  for (int i = 0; i < n; i++) {
+    double t = x[i];
+    for (int k = f[i]; k < i; k++) t -= L[i * n + k] * x[k];
+    x[i] = t / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double t = x[i];
+    for (int k = i + 1; k < n; k++)
+      if (f[k] <= i) t -= L[k * n + i] * x[k];
+    x[i] = t / L[i * n + i];
+  }
+}
+
 /* mj_setConst at qpos0: body_invweight0, dof_invweight0, meaninertia (engine_setconst.c set0) */
 void or_model_setconst(or_model* m) {
   or_data* d = or_data_create(m);

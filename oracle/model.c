@@ -214,7 +214,8 @@ void or_model_free(or_model* m) {
       (void**)&m->act_coef1, (void**)&m->act_gain, (void**)&m->act_bias, (void**)&m->act_ctrlrange,
       (void**)&m->act_forcerange, (void**)&m->eq_dof0, (void**)&m->eq_dof1, (void**)&m->eq_solref,
       (void**)&m->eq_solimp, (void**)&m->exclude, (void**)&m->qpos0, (void**)&m->arm_geom_lo,
-      (void**)&m->arm_geom_hi, (void**)&m->grip_site, (void**)&m->base_site, (void**)&m->cube_size};
+      (void**)&m->arm_geom_hi, (void**)&m->grip_site, (void**)&m->base_site, (void**)&m->cube_size, (void**)&m->cpair,
+      (void**)&m->run_lo, (void**)&m->run_geom, (void**)&m->run_body, (void**)&m->run_margin};
   for (size_t i = 0; i < sizeof fields / sizeof fields[0]; i++) free(*fields[i]);
   free(m);
 }
@@ -516,6 +517,7 @@ or_model* or_model_create(int A, int K, uint64_t seed) {
     else
       m->body_weldid[i] = m->body_weldid[m->body_parent[i]];
   }
+  or_collision_pairs(m);
   or_model_setconst(m);
   return m;
 }

@@ -67,6 +67,15 @@ typedef struct or_model {
   int bucket_geom[2];              /* target_area geoms */
   int cube_body0;                  /* body id of cube 0 */
   double *cube_size;               /* [K] half sizes */
+  /* geom pairs passing mj_collision's static filter (contype/conaffinity, weld/parent, excludes), type-ordered,
+   * g1 | g2 << 16, in its loop order: built once by or_collision_pairs so a substep only tests bounds */
+  int ncpair;
+  int *cpair;
+  /* runs of cpair sharing the loop's first geom and the second geom's body: [run_lo[r], run_lo[r + 1]) against
+   * geom run_geom[r] and body run_body[r], run_margin[r] the largest pair margin of the run */
+  int nrun;
+  int *run_lo, *run_geom, *run_body;
+  double *run_margin;
 } or_model;
 
 typedef struct or_contact {
@@ -106,6 +115,7 @@ void or_kinematics(const or_model* m, or_data* d);
 void or_mass(const or_model* m, or_data* d);
 void or_bias(const or_model* m, or_data* d);
 void or_collision(const or_model* m, or_data* d);
+void or_collision_pairs(or_model* m);
 void or_make_constraint(const or_model* m, or_data* d);
 void or_step1(const or_model* m, or_data* d);
 void or_step2(const or_model* m, or_data* d);

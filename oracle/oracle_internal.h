@@ -103,6 +103,8 @@ static inline void or_mulmm3(double* C, const double* A, const double* B) {
 void or_model_setconst(or_model* m);
 void or_cholesky(double* A, int n);                         /* in-place lower Cholesky, row-major n x n */
 void or_chol_solve(const double* L, int n, double* x);      /* solve L L^T x = b in place */
+void or_cholesky_env(double* A, int n, int* f);               /* the same factor, envelope f[] skipped (kin.c) */
+void or_chol_solve_env(const double* L, int n, const int* f, double* x);
 void or_body_jac(const or_model* m, const or_data* d, int body, const double p[3], double* jacp, double* jacr);
 void or_solve(const or_model* m, or_data* d);               /* Newton constraint solver (solver.c) */
 void or_fwd_actuation(const or_model* m, or_data* d);

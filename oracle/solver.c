@@ -198,6 +198,7 @@ void or_solve(const or_model* m, or_data* d) {
   memcpy(a, c_ws < c_sm ? d->qacc_warmstart : d->qacc_smooth, nv * sizeof(double));
   double cost = cost_at(m, d, a, jar, Ma);
   int it;
+  int nz[nv]; /* nonzero columns of a constraint row; then the Hessian's envelope */
   for (it = 0; it < OR_SOLVER_ITER; it++) {
     /* gradient and Hessian at a */
     memcpy(g, Ma, nv * sizeof(double));
@@ -206,18 +207,21 @@ void or_solve(const or_model* m, or_data* d) {
       if (!(d->efc_type[r] == OR_CNSTR_EQUALITY || jar[r] < 0)) continue;
       const double* J = d->efc_J + (size_t)r * nv;
       double Dr = d->efc_D[r];
-      for (int i = 0; i < nv; i++) {
-        if (J[i] == 0) continue;
+      int nnz = 0; /* the row's nonzero columns: the products with J[k] == 0 add exact zeros */
+      for (int i = 0; i < nv; i++)
+        if (J[i] != 0) nz[nnz++] = i;
+      for (int a_ = 0; a_ < nnz; a_++) {
+        const int i = nz[a_];
         g[i] += Dr * jar[r] * J[i];
-        for (int k = 0; k < nv; k++) H[i * nv + k] += Dr * J[i] * J[k];
+        for (int b_ = 0; b_ < nnz; b_++) H[i * nv + nz[b_]] += Dr * J[i] * J[nz[b_]];
       }
     }
     double gn = 0;
     for (int i = 0; i < nv; i++) gn += g[i] * g[i];
     if (scale * sqrt(gn) < OR_SOLVER_TOL) break;
-    or_cholesky(H, nv);
+    or_cholesky_env(H, nv, nz);
     for (int i = 0; i < nv; i++) dir[i] = -g[i];
-    or_chol_solve(H, nv, dir);
+    or_chol_solve_env(H, nv, nz, dir);
     /* exact line search along dir: f'(t) = c0 + c1 t on each active-set segment */
     double dMd = 0, dMa = 0;
     for (int i = 0; i < nv; i++) {

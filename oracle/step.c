@@ -79,9 +79,10 @@ void or_fwd_acceleration(const or_model* m, or_data* d) {
   for (int i = 0; i < nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
   double* L = d->scratch + 4 * nv * nv;
   memcpy(L, d->M, nv * nv * sizeof(double));
-  or_cholesky(L, nv);
+  int f[nv];
+  or_cholesky_env(L, nv, f);
   memcpy(d->qacc_smooth, d->qfrc_smooth, nv * sizeof(double));
-  or_chol_solve(L, nv, d->qacc_smooth);
+  or_chol_solve_env(L, nv, f, d->qacc_smooth);
 }
 
 static void fwd_constraint(const or_model* m, or_data* d) {
@@ -138,10 +139,11 @@ void or_implicit(const or_model* m, or_data* d) {
       for (int b = 0; b < 2; b++)
         if (dd[a] >= 0 && dd[b] >= 0) MhB[dd[a] * nv + dd[b]] -= dt * dv * cc[a] * cc[b];
   }
-  or_cholesky(MhB, nv);
+  int f[nv];
+  or_cholesky_env(MhB, nv, f);
   double* qa = d->scratch + 5 * nv * nv;
   for (int i = 0; i < nv; i++) qa[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
-  or_chol_solve(MhB, nv, qa);
+  or_chol_solve_env(MhB, nv, f, qa);
   if (g_acc_noise > 0)
     for (int i = 0; i < nv; i++) qa[i] *= 1.0 + g_acc_noise * noise_u();
   for (int i = 0; i < nv; i++) d->qvel[i] += dt * qa[i];
