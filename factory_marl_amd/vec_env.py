@@ -290,8 +290,15 @@ class FactoryVecEnv:
         return grid.transpose(0, 2, 1, 3, 4).reshape(rows * height, cols * width, 3)
 
     def seed(self, seed=None):
-        # seeds are fixed at creation (build_scene + TaskManager use the same seed, base_env.py:300,53)
-        return [None] * self.num_envs
+        """SB3 VecEnv.seed: per-env seeds seed + i for the next reset.  In the reference they reach
+        BaseEnv.reset_sim -> gymnasium's Env.reset(seed) (base_env.py:182), which seeds only gymnasium's
+        np_random; the scene (cube sizes) and the TaskManager RNG are seeded once at construction
+        (base_env.py:53, task_utils.py:19) and reset never reseeds them -- so, as there, the seeds recorded here
+        change no arena's trajectory (the per-arena seeds are fixed by fm_create)."""
+        if seed is None:
+            return [None] * self.num_envs
+        self._seeds = [int(seed) + i for i in range(self.num_envs)]
+        return list(self._seeds)
 
     def sync(self):
         _lib.check(self._L.fm_sync(self._h))
