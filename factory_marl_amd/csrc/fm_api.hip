@@ -72,6 +72,8 @@ struct fm_handle {
   int32_t* ints = nullptr;
   uint64_t* rng = nullptr;
   int64_t* counters = nullptr;
+  uint32_t* cost = nullptr;   // [N] last env-step duration per arena (s_memrealtime ticks)
+  int32_t* order = nullptr;   // [N] dispatch order of the next env-step, longest first
   unsigned long long* prof = nullptr;
   // rendering (fm_render): colour tables uploaded on first use, scratch grown on demand
   float* render_rgb = nullptr;   // [ngc][4]
@@ -171,6 +173,8 @@ static State<T> make_state(const fm_handle* h) {
   S.ints = h->ints;
   S.rng = h->rng;
   S.counters = h->counters;
+  S.cost = h->cost;
+  S.order = h->order;
   return S;
 }
 
@@ -310,6 +314,13 @@ static int create_typed(fm_handle* h) {
   HIPCHK(hipMalloc((void**)&h->counters, N * FM_NCTR * sizeof(int64_t)));
   h->allocs.push_back(h->counters);
   HIPCHK(hipMemset(h->counters, 0, N * FM_NCTR * sizeof(int64_t)));
+  if (!getenv("FACTORYSIM_NO_LPT")) {  // experiment switch: plain blockIdx -> arena dispatch
+    HIPCHK(hipMalloc((void**)&h->cost, N * sizeof(uint32_t)));
+    h->allocs.push_back(h->cost);
+    HIPCHK(hipMemset(h->cost, 0, N * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void**)&h->order, N * sizeof(int32_t)));
+    h->allocs.push_back(h->order);
+  }
   h->lay = lds_layout(d, sizeof(T));
   if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
   HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -399,8 +410,41 @@ static int set_state_typed(fm_handle* h, const char* src) {
   return FM_OK;
 }
 
+// Longest-processing-time-first order of the next env-step's workgroups: a counting sort of the arenas by
+// their last env-step duration (256 buckets of the range [0, max], longest first) in one workgroup.  The step
+// kernel runs N workgroups over a few hundred CUs several rounds deep; with the plain order the kernel ends when
+// the last expensive arena dispatched late finishes.  Order within a bucket is arbitrary (LDS atomics).
+__global__ void __launch_bounds__(1024) lpt_order_kernel(const uint32_t* __restrict__ cost, int32_t* __restrict__ order,
+                                                          int n) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned cmax;
+  const int t = (int)threadIdx.x;
+  if (t < 256) hist[t] = 0u;
+  if (t == 0) cmax = 0u;
+  __syncthreads();
+  unsigned m = 0u;
+  for (int i = t; i < n; i += (int)blockDim.x) m = cost[i] > m ? cost[i] : m;
+  atomicMax(&cmax, m);
+  __syncthreads();
+  const unsigned long long range = (unsigned long long)cmax + 1ull;
+  auto bucket = [&](int i) { return 255u - (unsigned)(((unsigned long long)cost[i] * 256ull) / range); };
+  for (int i = t; i < n; i += (int)blockDim.x) atomicAdd(&hist[bucket(i)], 1u);
+  __syncthreads();
+  if (t == 0) {
+    unsigned sum = 0u;
+    for (int b = 0; b < 256; b++) {
+      const unsigned c = hist[b];
+      hist[b] = sum;
+      sum += c;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += (int)blockDim.x) order[atomicAdd(&hist[bucket(i)], 1u)] = i;
+}
+
 template <typename T>
 static void launch_step(fm_handle* h, const StepIO& io) {
+  if (h->order) hipLaunchKernelGGL(lpt_order_kernel, dim3(1), dim3(1024), 0, h->stream, h->cost, h->order, h->dm.N);
   const StepParams<T> pd{make_model<T>(h), make_state<T>(h), h->lay, io};
   dim3 grid(h->dm.N), block(WAVE);
   const bool ik = h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS;

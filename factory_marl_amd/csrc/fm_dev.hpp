@@ -118,6 +118,10 @@ struct State {
   gptr<int32_t> ints;
   gptr<uint64_t> rng;      // [N][4]
   gptr<int64_t> counters;  // [N][4]
+  // dispatch order of the env-step (longest first, fm_api.hip lpt_order_kernel): workgroup b steps arena
+  // order[b]; cost[a] = arena a's last env-step in s_memrealtime ticks.  Null: workgroup b steps arena b.
+  gptr<uint32_t> cost{nullptr};
+  cptr<int32_t> order{nullptr};
 };
 
 struct StepIO {

@@ -3580,7 +3580,12 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
 #define S (kparams<StepParams<T>>().S)
 #define io (kparams<StepParams<T>>().io)
 #define L (kparams<StepParams<T>>().L)
-  const int arena = blockIdx.x;
+  // longest-processing-time-first dispatch: the host orders the arenas by their last env-step's duration, so the
+  // expensive ones start in the first wave of workgroups and the cheap ones fill the tail (results do not depend
+  // on which workgroup steps an arena)
+  const int32_t* const order_ = S.order;
+  const int arena = order_ ? order_[blockIdx.x] : (int)blockIdx.x;
+  const unsigned long long t_begin = wall_clock64();
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K, nu = dm.nu;
   // a fresh opaque LDS base per use: workspace addresses are recomputed inside each phase instead of
@@ -3785,6 +3790,10 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   if (io.obs) write_obs(M, w, ti, td, io.obs + (size_t)arena * dm.obs_dim);
   PMARK(PH_TAIL);
   if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);
+  {
+    uint32_t* const cost_ = S.cost;
+    if (cost_ && LANE == 0) cost_[arena] = (uint32_t)(wall_clock64() - t_begin);
+  }
 #undef ctrl_
 #undef uctl_
 #undef sc_
