@@ -62,3 +62,23 @@ def test_alternating_streams_match_single_stream():
         got = env.get_state()
     env.close()
     assert np.array_equal(got, want)
+
+
+def test_longest_first_dispatch_does_not_change_results(monkeypatch):
+    """the env-step's workgroup -> arena map is re-sorted every step by the arenas' last durations
+    (lpt_order_kernel); stepping with it and with the plain blockIdx order
+    (FACTORYSIM_NO_LPT, read at fm_create) gives the same observations and arena state bit for bit"""
+    n, steps = 512, 40
+    lpt = _env(n)
+    monkeypatch.setenv("FACTORYSIM_NO_LPT", "1")
+    plain = _env(n)
+    monkeypatch.delenv("FACTORYSIM_NO_LPT")
+    for a in _actions(n, steps, lpt.device):
+        lpt.step_tensors(a)
+        plain.step_tensors(a)
+    lpt.sync()
+    plain.sync()
+    assert torch.equal(lpt.obs, plain.obs)
+    assert np.array_equal(lpt.get_state(), plain.get_state())
+    lpt.close()
+    plain.close()
