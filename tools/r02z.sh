@@ -2,7 +2,7 @@
 # final round-2 check of the committed tree: full GPU suite (oracle checker rebuilt with the faster collision /
 # envelope Cholesky), smoke, default bench with the CPU-baseline leg
 set -o pipefail
-O=gpurun_out/r02z
+O=gpurun_out/${R02Z_TAG:-r02z}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 400 --timeout-method thread > $O/tests.log 2>&1 || { echo "GPU SUITE FAILED"; tail -30 $O/tests.log; exit 1; }
