@@ -21,6 +21,12 @@ kernel is bound by neither HBM nor MFMA but by dependent LDS / VALU latency chai
 fp32 vector peak with the live kernel time.
 CPU baseline: the oracle (our C restatement of the reference algorithm, oracle/) stepped with OpenMP on
 the host cores of the same box, on a bounded sample, rank 0 at N=1 only.
+
+Launch: ``python bench.py --gpus N`` starts N rank processes itself (the parent touches no GPU; RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* at 127.0.0.1, one GPU each) and prints rank 0's line; under torchrun (WORLD_SIZE set) the
+process is one rank and --gpus must equal WORLD_SIZE.  --scaling weak (default): --arenas per GPU; strong: --arenas
+is the job total, split over the ranks.  --workload config4: 131072 arenas (2,8) strong-split over the ranks with
+the PPO rollout + RCCL update of config 3.
 """
 import argparse
 import json
@@ -32,6 +38,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from factory_marl_amd.environments import run_kwargs  # noqa: E402
 from factory_marl_amd.launch import (RankContext, arena_seeds, job_throughput, max_over_ranks,  # noqa: E402,F401
                                      rank_arenas)
 
@@ -112,7 +119,8 @@ def timed_run(ctx, args, precision, steps, warmup, lo, hi):
     from factory_marl_amd import FactoryVecEnv
 
     A, K, N = args.arms, args.objects, hi - lo
-    env = FactoryVecEnv(N, env_class=args.env_class, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42),
+    env = FactoryVecEnv(N, env_class=args.env_class,
+                        env_kwargs=run_kwargs(args.env_class, num_arms=A, max_num_objects=K, seed=42),
                         device=ctx.local_rank, precision=precision, seeds=arena_seeds(lo, hi, args.seeds))
     env.reset()
     preroll(env, args.preroll, ctx.rank, ctx.device)
@@ -153,7 +161,8 @@ def timed_run_ppo(ctx, args, lo, hi):
     from factory_marl_amd.ppo import PPO
 
     A, K, N = args.arms, args.objects, hi - lo
-    env = FactoryVecEnv(N, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42), device=ctx.local_rank,
+    env = FactoryVecEnv(N, env_kwargs=run_kwargs(args.env_class, num_arms=A, max_num_objects=K, seed=42),
+                        device=ctx.local_rank,
                         precision=args.precision, seeds=arena_seeds(lo, hi, args.seeds))
     env.reset()
     preroll(env, args.preroll, ctx.rank, ctx.device)
@@ -207,9 +216,90 @@ def load_json(path):
         return None
 
 
+def free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` without a torchrun environment: N rank processes of this script, one GPU each, 127.0.0.1
+    rendezvous.  The parent never touches the GPU (it only waits), so nothing is exec'd from a GPU process; rank 0
+    prints the JSON line.  Returns the first non-zero rank exit code (the other ranks are then stopped)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def resolve_world(args):
+    """None = run in this process; otherwise the exit code of the spawned ranks"""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            return spawn_ranks(args.gpus, sys.argv[1:])
+        args.gpus = 1
+        return None
+    w = int(env_world)
+    if args.gpus is None:
+        args.gpus = w
+    if args.gpus != w:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={w}")
+    return None
+
+
+def main_dry_run(args):
+    """the launch path without a GPU (tests/test_distributed.py): gloo ranks, the arena partition and the
+    max-over-ranks clock of the real run, a synthetic wall time per rank"""
+    import torch.distributed as dist
+
+    ctx = RankContext.from_env(use_gpu=False)
+    lo, hi = rank_arenas(args.arenas, ctx.world, ctx.rank, args.scaling)
+    ranges = [None] * ctx.world
+    if ctx.distributed:
+        dist.all_gather_object(ranges, (lo, hi))
+    else:
+        ranges = [(lo, hi)]
+    wall = ctx.max_over_ranks(1.0 + 0.5 * ctx.rank)
+    total = ctx.sum_over_ranks(hi - lo)
+    if ctx.rank == 0:
+        print(json.dumps({"metric": "dry run (launcher only)", "n_gpus": ctx.world, "scaling": args.scaling,
+                          "backend": ctx.backend, "rank_arenas": [list(r) for r in ranges], "total_arenas": int(total),
+                          "wall_max": wall, "value": total * args.steps / wall}), flush=True)
+    ctx.close()
+
+
+def job_arenas(args, world):
+    """arenas stepped by the whole job"""
+    return args.arenas * world if args.scaling == "weak" else args.arenas
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --arenas per GPU; strong: --arenas for the whole job, split over the ranks")
+    ap.add_argument("--dry-run", action="store_true", help="launcher / partition only, no GPU (tests)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--arenas", type=int, default=4096, help="arenas per GPU")
@@ -226,30 +316,42 @@ def main():
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "pmc_valu.json"),
                     help="VALU instruction counts per arena env-step by rocprofv3 --pmc (tools/pmc_valu.py)")
-    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config5"],
-                    help="config2: the headline (random policy); config3: 16384 arenas 2x8 PPO rollout; config5: "
+    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config4", "config5"],
+                    help="config2: the headline (random policy); config3: 16384 arenas 2x8 PPO rollout; config4: "
+                         "131072 arenas 2x8 PPO rollout strong-split over the ranks (RCCL update); config5: "
                          "4 arms x 16 objects PauseIKToggleEnv, 4096 arenas per GPU (32768 on 8), random toggles")
     ap.add_argument("--ppo-batch", type=int, default=16384)
     ap.add_argument("--ppo-epochs", type=int, default=10)
     args = ap.parse_args()
     args.env_class = "AllFullRLProgressRewardEnv"
-    if args.workload == "config3":
+    if args.workload == "config4":
+        if args.arenas == 4096:
+            args.arenas = 131072
+        args.scaling = "strong"
+    rc = resolve_world(args)
+    if rc is not None:
+        return rc
+    if args.dry_run:
+        return main_dry_run(args)
+    if args.workload in ("config3", "config4"):
         return main_config3(args)
     if args.workload == "config5":
         return main_config5(args)
 
     ctx = RankContext.from_env()
-    A, K, N = args.arms, args.objects, args.arenas
-    lo, hi = rank_arenas(N, ctx.world, ctx.rank, "weak")
+    A, K = args.arms, args.objects
+    lo, hi = rank_arenas(args.arenas, ctx.world, ctx.rank, args.scaling)
+    N = hi - lo  # this rank's arenas
+    NJ = job_arenas(args, ctx.world)
     wall, kern_ms, dc = timed_run(ctx, args, args.precision, args.steps, args.warmup, lo, hi)
     wall = ctx.max_over_ranks(wall)
-    value = job_throughput(N, args.steps, ctx.world, wall)
+    value = NJ * args.steps / wall
     diag = diagnostics(dc, N, args.steps)
     fp64 = None
     if args.fp64_steps > 0 and args.precision == "fp32":
         w64, k64, dc64 = timed_run(ctx, args, "fp64", args.fp64_steps, min(args.warmup, 5), lo, hi)
         w64 = ctx.max_over_ranks(w64)
-        fp64 = {"value": round(job_throughput(N, args.fp64_steps, ctx.world, w64), 2), "steps": args.fp64_steps,
+        fp64 = {"value": round(NJ * args.fp64_steps / w64, 2), "steps": args.fp64_steps,
                 "ms_per_step": round(w64 / args.fp64_steps * 1e3, 4), "kernel_ms_avg": round(k64, 4),
                 "diagnostics": diagnostics(dc64, N, args.fp64_steps)}
     if ctx.rank == 0:
@@ -285,14 +387,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": f"synthetic (random U[-1,1] AllFullRL actions, Philox seed 0+rank; scene seed "
                     f"{'42' if args.seeds == 'fixed' else '42+arena id'}; {args.preroll}-step desynchronising pre-roll)",
             "config": {"workload": f"config 2: {N} arenas/GPU, {A} arms x {K} objects, AllFullRLProgressRewardEnv, "
                                    "random policy, 100 substeps/env-step, auto-reset, stationary episode mix",
-                       "arenas_per_gpu": N, "num_arms": A, "max_num_objects": K,
+                       "arenas_per_gpu": N, "job_arenas": NJ, "num_arms": A, "max_num_objects": K,
                        "parallelism": f"arena-sharded x{ctx.world} (no collective)"},
             "roofline": roof,
             "diagnostics": diag,
@@ -316,17 +418,18 @@ def main_config5(args):
     if args.preroll == 200:
         args.preroll = 100
     ctx = RankContext.from_env()
-    A, K, N = args.arms, args.objects, args.arenas
-    lo, hi = rank_arenas(N, ctx.world, ctx.rank, "weak")
+    A, K = args.arms, args.objects
+    lo, hi = rank_arenas(args.arenas, ctx.world, ctx.rank, args.scaling)
+    N = hi - lo
     wall, kern_ms, dc = timed_run(ctx, args, args.precision, args.steps, args.warmup, lo, hi)
     wall = ctx.max_over_ranks(wall)
-    value = job_throughput(N, args.steps, ctx.world, wall)
+    value = job_arenas(args, ctx.world) * args.steps / wall
     if ctx.rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), 4096 arenas/GPU 4-arm x 16-obj PauseIKToggleEnv; MI355X",
             "value": round(value, 2), "unit": "env-steps/s", "n_gpus": ctx.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f64",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": f"synthetic (fair-coin MultiDiscrete toggles, Philox seed 0+rank; scene seed 42; {args.preroll}-step "
                     "desynchronising pre-roll)",
             "config": {"workload": f"config 5: {N} arenas/GPU, {A} arms x {K} objects, PauseIKToggleEnv (float64 IK "
@@ -342,7 +445,10 @@ def main_config5(args):
 
 def main_config3(args):
     """BASELINE config 3: 16384 arenas, 2 arms x 8 objects, PPO rollout with the PyTorch-ROCm policy, 1 MI355X
-    (per GPU with --gpus N: weak scaling, gradient / advantage all-reduce in the PPO update only)"""
+    (per GPU with --gpus N: weak scaling, gradient / advantage all-reduce in the PPO update only).
+    BASELINE config 4 (--workload config4): 131072 arenas of the same scene strong-split over the ranks
+    (16384 per GPU on 8), the same PPO rollout, the update's gradient and advantage all-reduces over RCCL"""
+    c4 = args.workload == "config4"
     if args.arenas == 4096:
         args.arenas = 16384
     if args.objects == 4:
@@ -352,28 +458,37 @@ def main_config3(args):
     if args.warmup == 10:
         args.warmup = 2
     ctx = RankContext.from_env()
-    A, K, N = args.arms, args.objects, args.arenas
-    lo, hi = rank_arenas(N, ctx.world, ctx.rank, "weak")
+    A, K = args.arms, args.objects
+    lo, hi = rank_arenas(args.arenas, ctx.world, ctx.rank, args.scaling)
+    N = hi - lo
+    NJ = job_arenas(args, ctx.world)
     wall, train_s, dc = timed_run_ppo(ctx, args, lo, hi)
     wall = ctx.max_over_ranks(wall)
     train_s = ctx.max_over_ranks(train_s)
-    value = job_throughput(N, args.steps, ctx.world, wall)
+    value = NJ * args.steps / wall
+    samples = NJ * args.steps
     if ctx.rank == 0:
+        name = "config 4" if c4 else "config 3"
         line = {
-            "metric": "env-steps/sec (whole node), 16384 arenas 2-arm×8-obj PPO rollout; MI355X",
+            "metric": (f"env-steps/sec (whole node), {NJ} arenas 2-arm×8-obj PPO rollout sharded over {ctx.world} "
+                       "MI355X" if c4 else "env-steps/sec (whole node), 16384 arenas 2-arm×8-obj PPO rollout; MI355X"),
             "value": round(value, 2), "unit": "env-steps/s", "n_gpus": ctx.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f64",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": "synthetic: PPO rollout of a freshly initialised MlpPolicy [128, 128] (SB3 init), Gaussian "
-                    f"sampling; scene seed 42; {args.preroll}-step desynchronising pre-roll",
-            "config": {"workload": f"config 3: {N} arenas/GPU, {A} arms x {K} objects, AllFullRLProgressRewardEnv, "
-                                   "PPO rollout (policy forward + sampling + env-step + buffer writes timed)",
-                       "arenas_per_gpu": N, "num_arms": A, "max_num_objects": K,
+                    f"sampling (per-rank stream); scene seed 42; {args.preroll}-step desynchronising pre-roll",
+            "config": {"workload": f"{name}: {N} arenas/GPU ({NJ} in the job), {A} arms x {K} objects, "
+                                   "AllFullRLProgressRewardEnv, PPO rollout (policy forward + sampling + env-step + "
+                                   "buffer writes timed)",
+                       "arenas_per_gpu": N, "job_arenas": NJ, "num_arms": A, "max_num_objects": K,
                        "parallelism": f"arena-sharded x{ctx.world}; RCCL all-reduce in the update only"},
-            "ppo_update": {"seconds": round(train_s, 4), "samples": N * args.steps * ctx.world,
-                           "samples_per_s": round(N * args.steps * ctx.world / train_s, 1),
-                           "n_epochs": args.ppo_epochs, "batch_size_per_rank": args.ppo_batch},
-            "iteration_env_steps_per_s": round(N * args.steps * ctx.world / (wall + train_s), 2),
+            "ppo_update": {"seconds": round(train_s, 4), "samples": samples,
+                           "samples_per_s": round(samples / train_s, 1),
+                           "n_epochs": args.ppo_epochs, "batch_size_per_rank": args.ppo_batch,
+                           "collectives": ("per minibatch: async all-reduce of the advantage statistics + one fused "
+                                           "gradient all-reduce; per rollout: episode statistics"
+                                           if ctx.world > 1 else "none (1 rank)")},
+            "iteration_env_steps_per_s": round(samples / (wall + train_s), 2),
             "diagnostics": diagnostics(dc, N, args.steps),
         }
         print(json.dumps(line), flush=True)
@@ -381,4 +496,4 @@ def main_config3(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

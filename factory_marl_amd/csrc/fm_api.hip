@@ -138,6 +138,14 @@ static Model<T> make_model(const fm_handle* h) {
   M.env_class = c.env_class;
   M.solver_iter = c.solver_iterations;
   M.solver_tol = c.solver_tolerance;
+  {
+    const double dt = 0.001 * h->dm.frame_skip;  // env.dt = model.opt.timestep * frame_skip (base_env.py:201-202)
+    M.ik_time.pt_comp = c.pt_time * dt * 15.0;
+    M.ik_time.release_wait = (int)(0.5 / dt);
+    M.ik_time.grasp_wait = (int)(1.0 / dt);
+    M.ik_time.move_steps = (int)(1.0 / dt);
+    M.ik_time.timeout_steps = (int)(3.0 / dt);
+  }
   M.arm_base = (const T*)h->arm_base;
   M.arm_base_w = h->arm_base_w;
   M.body = (const T*)h->body;
@@ -160,8 +168,7 @@ static Model<T> make_model(const fm_handle* h) {
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
   const char* cl = getenv("FM_CHOL_LDS");
-  const char* ng = getenv("FM_NO_NOISE_GUARD");  // experiments: fp32 Newton without the cost-noise stop
-  M.dbg_flags = ((cl && cl[0] == '1') ? 1 : 0) | ((ng && ng[0] == '1') ? 2 : 0);
+  M.dbg_flags = (cl && cl[0] == '1') ? 1 : 0;
   return M;
 }
 
@@ -536,10 +543,12 @@ void fm_config_default(fm_config* c) {
   c->control_frequency = 10;
   c->spawn_freq = 1.0 / 10;
   c->spawn_freq_increase = 1.001;
-  c->gripper_to_closest_cube_reward_factor = 0.2;
-  c->closest_cube_to_bucket_reward_factor = 0.4;
+  // ProgressRewardEnv (environments.py:252-258): the three factors are required keyword arguments there (no
+  // reference default; the caller sets them), base_reward defaults to 0
+  c->gripper_to_closest_cube_reward_factor = 0.0;
+  c->closest_cube_to_bucket_reward_factor = 0.0;
   c->small_action_norm_reward_factor = 0.0;
-  c->base_reward = 0.4;
+  c->base_reward = 0.0;
   c->solver_iterations = 100;
   c->solver_tolerance = 0.0;  // 0 = precision default (see fm_create)
 }
@@ -648,6 +657,48 @@ int fm_set_stream(fm_handle* h, void* stream) {
   HIPCHK(hipEventRecord(h->handoff, h->stream));
   HIPCHK(hipStreamWaitEvent(next, h->handoff, 0));
   h->stream = next;
+  return FM_OK;
+}
+
+// runtime-mutable scalars of the reference env (set_attr / get_attr): fields of the handle's config, read by every
+// later launch's Model (make_model runs per launch, so a change is ordered with the queued work)
+static double* param_slot(fm_handle* h, const char* name, double* scale) {
+  *scale = 1.0;
+  if (!name) return nullptr;
+  fm_config& c = h->cfg;
+  const std::string n(name);
+  if (n == "pt_time") return &c.pt_time;
+  if (n == "initial_conveyor_speed") return &c.initial_conveyor_speed;
+  if (n == "conveyor_acceleration") return &c.conveyor_acceleration;
+  if (n == "force_contact_threshold") return &c.force_contact_threshold;
+  if (n == "spawn_freq_increase") return &c.spawn_freq_increase;
+  if (n == "init_spawn_freq") {  // BaseEnv.init_spawn_freq = spawn_freq * num_arms (base_env.py:36, 139)
+    *scale = (double)h->dm.A;
+    return &c.spawn_freq;
+  }
+  if (n == "gripper_to_closest_cube_reward_factor") return &c.gripper_to_closest_cube_reward_factor;
+  if (n == "closest_cube_to_bucket_reward_factor") return &c.closest_cube_to_bucket_reward_factor;
+  if (n == "small_action_norm_reward_factor") return &c.small_action_norm_reward_factor;
+  if (n == "base_reward") return &c.base_reward;
+  return nullptr;
+}
+
+int fm_set_param(fm_handle* h, const char* name, double value) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  double scale;
+  double* p = param_slot(h, name, &scale);
+  if (!p) return set_err(FM_EINVAL, std::string("not a runtime-mutable parameter: ") + (name ? name : "(null)"));
+  if (!std::isfinite(value)) return set_err(FM_EINVAL, "non-finite value");
+  *p = value / scale;
+  return FM_OK;
+}
+
+int fm_get_param(const fm_handle* h, const char* name, double* value) {
+  if (!h || !value) return set_err(FM_EINVAL, "null argument");
+  double scale;
+  double* p = param_slot(const_cast<fm_handle*>(h), name, &scale);
+  if (!p) return set_err(FM_EINVAL, std::string("not a runtime-mutable parameter: ") + (name ? name : "(null)"));
+  *value = *p * scale;
   return FM_OK;
 }
 

@@ -73,6 +73,13 @@ struct Dims {
 // indices into the int block after the two lists
 enum { I_NIN = 0, I_NOUT, I_STEP, I_SINCE, I_FAIL, I_HIDDEN, I_S0, I_S1, I_LS0, I_LS1, I_EPLEN, I_NINT };
 
+// IKPolicy's step counts and velocity compensation (ik_policy.py:56-67), from env.dt = timestep * frame_skip and
+// env.pt_time on the host: int(0.5 / dt), int(1 / dt), int(1 / dt), int(3 / dt), pt_time * dt * 15
+struct IkTiming {
+  double pt_comp;
+  int release_wait, grasp_wait, move_steps, timeout_steps;
+};
+
 template <typename T>
 struct Model {
   Dims dm;
@@ -84,6 +91,7 @@ struct Model {
   double bucket_x0, bucket_x1, bucket_y, bucket_z;
   int env_class, solver_iter;
   double solver_tol;
+  IkTiming ik_time;
   // arm template
   cptr<T> arm_base;  // [A][12]  world pos(3), R(9) of the iiwa frame (kernel frame: zshift)
   cptr<double> arm_base_w;  // [A][12] the same in float64, world frame (IK base policy, fm_ik.hpp)
@@ -107,8 +115,7 @@ struct Model {
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
-  int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one, bit 1 = no fp32
-                             // cost-noise stop in Newton (FM_NO_NOISE_GUARD=1)
+  int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one (FM_CHOL_LDS=1)
 };
 
 template <typename T>
@@ -210,12 +217,29 @@ __host__ __device__ constexpr double zshift() {
 }
 
 // per-contact real record; the Jacobian block first, so its three rows of CJ (even) start 8-byte aligned
-// (records are CR_N = 84 reals, a multiple of 16 bytes) and read as 64-bit LDS loads
-enum { CR_J = 0, CR_DIST = CR_J + 3 * CJ, CR_MU, CR_D, CR_KD, CR_BD, CR_POS, CR_FR = CR_POS + 3, CR_VEL = CR_FR + 9,
-       CR_JA = CR_VEL + 3, CR_JD = CR_JA + 3, CR_F = CR_JD + 3, CR_N = CR_F + 4,
-       CR_K = CR_JD /* 6 slots over JD+F: K_c during the Hessian build only */ };
-// generic row record (equality / joint limit)
-enum { RR_C0 = 0, RR_C1, RR_POS, RR_D, RR_AREF, RR_JAR, RR_JD, RR_F, RR_N };
+// (records are CR_N = 84 reals, a multiple of 16 bytes) and read as 64-bit LDS loads.
+// The Newton solver's per-contact iterate products are float64 in both builds (dslot(): CR_JA = B a and CR_JD =
+// B dir, 3 doubles each; CR_F3 = the frame force D jar summed over the active edges, 3 doubles).  In the fp32
+// record a double takes two slots: JA / JD overlay the contact geometry (dist, pos, frame: 13 slots, consumed
+// when the rows are built), F3 shares its 6 slots with K_c (Hessian build only); every double starts on an
+// even slot (8-byte aligned).
+enum { CR_J = 0, CR_DIST = CR_J + 3 * CJ, CR_POS, CR_FR = CR_POS + 3, CR_MU = CR_FR + 9, CR_D, CR_KD, CR_BD, CR_VEL,
+       CR_F3 = CR_VEL + 3, CR_F = CR_F3 + 6, CR_N = CR_F + 4,
+       CR_JA = CR_DIST, CR_JD = CR_DIST + 6, CR_K = CR_F3 };
+static_assert(CR_JA % 2 == 0 && CR_JD % 2 == 0 && CR_F3 % 2 == 0 && CR_JD + 6 <= CR_MU && CR_N % 4 == 0,
+              "contact record: float64 slots aligned, JA / JD inside the geometry slots");
+// generic row record (equality / joint limit); JAR = J a - aref and JD = J dir are float64 slots (2 reals in fp32)
+enum { RR_C0 = 0, RR_C1, RR_POS, RR_D, RR_AREF, RR_F, RR_JAR, RR_JD = RR_JAR + 2, RR_N = RR_JD + 2 };
+static_assert(RR_JAR % 2 == 0 && RR_N % 2 == 0, "row record: float64 slots aligned");
+// float64 view of a record slot (both builds)
+template <typename T>
+__host__ __device__ __forceinline__ double* dslot(T* rec, int k) {
+  return (double*)(rec + k);
+}
+template <typename T>
+__host__ __device__ __forceinline__ const double* dslot(const T* rec, int k) {
+  return (const double*)(rec + k);
+}
 // phase slots of the optional wall-clock profile (fm_profile)
 enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_NHESS, PH_NCHOL, PH_NSOLVE, PH_NLS,
        PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_LAST };
@@ -326,6 +350,41 @@ __device__ __forceinline__ float wave_min(float x) {
   x = fminf(x, dpp_f32<0x143>(x, x));
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
+// fp64 reductions (the Newton solver's cost, gradient and line search in both builds): the same DPP sequence
+// moving both 32-bit halves, then the 64-bit read of lane 63
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x, double old) {
+  const unsigned long long xi = (unsigned long long)__double_as_longlong(x);
+  const unsigned long long oi = (unsigned long long)__double_as_longlong(old);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)oi, (int)(unsigned)xi, CTRL, 0xf, 0xf, false);
+  const unsigned hi =
+      (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(oi >> 32), (int)(unsigned)(xi >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double lane63_f64(double x) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_sum(double x) {
+  x += dpp_f64<0xb1>(x, 0.0);
+  x += dpp_f64<0x4e>(x, 0.0);
+  x += dpp_f64<0x124>(x, 0.0);
+  x += dpp_f64<0x128>(x, 0.0);
+  x += dpp_f64<0x142>(x, 0.0);
+  x += dpp_f64<0x143>(x, 0.0);
+  return lane63_f64(x);
+}
+__device__ __forceinline__ double wave_min(double x) {
+  x = fmin(x, dpp_f64<0xb1>(x, x));
+  x = fmin(x, dpp_f64<0x4e>(x, x));
+  x = fmin(x, dpp_f64<0x124>(x, x));
+  x = fmin(x, dpp_f64<0x128>(x, x));
+  x = fmin(x, dpp_f64<0x142>(x, x));
+  x = fmin(x, dpp_f64<0x143>(x, x));
+  return lane63_f64(x);
+}
 
 // inclusive prefix sum of an int over the wave on DPP (row shifts, then the row broadcasts; rocPRIM's
 // warp_scan_dpp sequence); full wave active at every call site
@@ -377,15 +436,12 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.bc = take(tsize * WAVE);
   L.q = take(tsize * nq);
   L.v = take(tsize * nv);
-  L.a = take(tsize * nv);
+  L.a = take(8 * nv);  // Newton iterate (float64 in both builds; the next substep's warmstart)
   L.as = take(tsize * nv);
   L.fs = take(tsize * nv);
   L.fc = take(tsize * nv);
   L.pb = take(tsize * nv);
-  L.g = take(tsize * nv);
   L.dir = take(tsize * nv);
-  L.Ma = take(tsize * nv);
-  L.tmp = take(tsize * nv);
   L.fa = take(tsize * nv);
   // float64 master state: the fp32 physics reads the float copies q / v, the integrator accumulates in
   // double (an fp32 qpos cannot absorb increments below half an ulp: dt * qvel of a joint at rest)
@@ -408,10 +464,14 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.cbi = take(4 * 4 * ncb);
   L.cbg = take(2 * ngc);
   L.cube = take(tsize * 4 * K);
-  // phase-local buffers share one region: collision work lists (stage) and the Newton Hessian (solve)
-  // are never live together
+  // phase-local buffers share one region: collision work lists (stage) and the Newton Hessian + the solver's
+  // float64 vectors (gradient, M (a - as), scratch; live from the solve to the integration) are never live
+  // together
   const int u0 = off;
   L.H = take(tsize * nv * nv);
+  L.g = take(8 * nv);
+  L.Ma = take(8 * nv);
+  L.tmp = take(8 * nv);
   int uend = off;
   off = u0;
   L.gx = take(tsize * 4 * ngc);

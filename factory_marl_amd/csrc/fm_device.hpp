@@ -87,12 +87,12 @@ struct Ws {
       return (T*)(base + L->v);
     }
   }
-  __device__ __forceinline__ T* a() const {
+  __device__ __forceinline__ double* a() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.a);
+      return (double*)(base + c.a);
     } else {
-      return (T*)(base + L->a);
+      return (double*)(base + L->a);
     }
   }
   __device__ __forceinline__ T* as() const {
@@ -127,12 +127,12 @@ struct Ws {
       return (T*)(base + L->pb);
     }
   }
-  __device__ __forceinline__ T* g() const {
+  __device__ __forceinline__ double* g() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.g);
+      return (double*)(base + c.g);
     } else {
-      return (T*)(base + L->g);
+      return (double*)(base + L->g);
     }
   }
   __device__ __forceinline__ T* dir() const {
@@ -143,20 +143,20 @@ struct Ws {
       return (T*)(base + L->dir);
     }
   }
-  __device__ __forceinline__ T* Ma() const {
+  __device__ __forceinline__ double* Ma() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.Ma);
+      return (double*)(base + c.Ma);
     } else {
-      return (T*)(base + L->Ma);
+      return (double*)(base + L->Ma);
     }
   }
-  __device__ __forceinline__ T* tmp() const {
+  __device__ __forceinline__ double* tmp() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.tmp);
+      return (double*)(base + c.tmp);
     } else {
-      return (T*)(base + L->tmp);
+      return (double*)(base + L->tmp);
     }
   }
   __device__ __forceinline__ T* fa() const {
@@ -1553,6 +1553,9 @@ __device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T, DIM>
   }
 }
 
+template <typename O, typename T, typename DIM, typename X>
+__device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& w, const X* x, int ncon, int slot);
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
   const DIM dm(M.dm);
@@ -1795,7 +1798,7 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   }
   SYNC();
   // efc velocity in the contact frame
-  contact_jx(M, w, v, ncon, CR_VEL);
+  contact_jx<T>(M, w, v, ncon, CR_VEL);
   // ---- generic rows: gripper joint equality + active joint limits.  One candidate row per lane in the
   // reference's order (per arm: the equality, then each dof's lower and upper limit), compacted by ballot
   {
@@ -1889,20 +1892,21 @@ __device__ __forceinline__ T Mdiag(const Model<T>& M, const Ws<T, DIM>& w, int i
   return r < 3 ? c[1] : c[2];
 }
 
-// out = M x   (lanes over dofs)
-template <typename T, typename DIM>
-__device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T, DIM>& w, int arena, const T* x, T* out) {
+// out = M x   (lanes over dofs), accumulated in out's type (the solver's float64 vectors: M's float entries
+// times float or double operands)
+template <typename T, typename DIM, typename X, typename O>
+__device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T, DIM>& w, int arena, const X* x, O* out) {
   const DIM dm(M.dm);
   int a0 = 1 + 6 * dm.K;
   for (int i = LANE; i < dm.nv; i += WAVE) {
     if (i < a0) {
-      out[i] = Mdiag(M, w, i) * x[i];
+      out[i] = (O)Mdiag(M, w, i) * (O)x[i];
     } else {
       int arm = (i - a0) / 9, r = (i - a0) % 9;
       const T* Mb = w.Marm() + 81 * arm + 9 * r;
-      const T* xa = x + a0 + 9 * arm;
-      T s = 0;
-      for (int j = 0; j < 9; j++) s += Mb[j] * xa[j];
+      const X* xa = x + a0 + 9 * arm;
+      O s = 0;
+      for (int j = 0; j < 9; j++) s += (O)Mb[j] * (O)xa[j];
       out[i] = s;
     }
   }
@@ -1984,11 +1988,12 @@ __device__ __forceinline__ void contact_K(const Ws<T, DIM>& w, int ncon) {
     T* cr = w.cr() + CR_N * c;
     const T mu = cr[CR_MU], D = cr[CR_D], bd = cr[CR_BD], kd = cr[CR_KD];
     T Kc[6] = {0, 0, 0, 0, 0, 0};
+    const double* ja = dslot(cr, CR_JA);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
-      const T jar = edge_val(cr + CR_JA, mu, e) - aref;
-      if (jar < T(0)) {
+      const double jar = edge_val(ja, (double)mu, e) - (double)aref;  // the active set of the float64 cost
+      if (jar < 0.0) {
         const T sg = (e & 1) ? -mu : mu;
         Kc[0] += D;
         if (e < 2) {
@@ -2016,7 +2021,7 @@ __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_
 //    the fill-in of this elimination order) comes from the tree->contact masks; a pivot updates only the row
 //    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
 template <typename T, typename DIM>
-__device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const T* g,
+__device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
                                                T* dir) {
   constexpr int NV = DIM::nv, KK = DIM::K, AA = DIM::A, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
   const int j = LANE;
@@ -2095,7 +2100,7 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
       });
     }
   });
-  T acc = j < NV ? -g[jo] : T(0);
+  T acc = j < NV ? (T)-g[jo] : T(0);
   T y = T(0);
 #pragma unroll
   for (int k = 0; k < NV; k++) {
@@ -2134,7 +2139,7 @@ __device__ constexpr bool border_chol() {
 typedef float fm_f32x4 __attribute__((ext_vector_type(4)));
 template <typename DIM>
 __device__ __forceinline__ void chol_sparse_border(const Model<float>& M, const Ws<float, DIM>& w, float* H,
-                                                   const float* g, float* dir) {
+                                                   const double* g, float* dir) {
   constexpr int NV = DIM::nv, KK = DIM::K, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
   constexpr int NH = WAVE, NB = NV - WAVE, NW = (DIM::MAXC + 63) / 64;
   static_assert(NB > 0 && NB <= 16, "border of at most 16 positions");
@@ -2262,7 +2267,7 @@ __device__ __forceinline__ void chol_sparse_border(const Model<float>& M, const 
     }
   }
   // ---- forward: head, then the border rows (their sums over the head columns from LDS)
-  float acc = -g[jo];
+  float acc = (float)-g[jo];
   float y = 0.0f;
 #pragma unroll
   for (int k = 0; k < NH; k++) {
@@ -2279,7 +2284,7 @@ __device__ __forceinline__ void chol_sparse_border(const Model<float>& M, const 
     float sum = 0.0f;
 #pragma unroll 16
     for (int k = 0; k < NH; k++) sum += LB[16 * k + j] * ys[k];
-    accb = -g[dof_of(NH + j)] - sum;
+    accb = (float)-g[dof_of(NH + j)] - sum;
   }
   float yb = 0.0f;
 #pragma unroll
@@ -2320,12 +2325,12 @@ __device__ __forceinline__ void chol_sparse_border(const Model<float>& M, const 
 // its column.  The substitutions walk the same row sets.  Returns false (nothing written) when the scene has more
 // trees than a 32-bit coupling mask holds.
 template <typename T, typename DIM>
-__device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, DIM>& w, T* H, const T* g, T* dir) {
+__device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, DIM>& w, T* H, const double* g, T* dir) {
   const DIM dm(M.dm);
   const int NV = dm.nv, K = dm.K, NT = dm.ntree, A0 = 1 + 6 * K;
   if (NT > 32) return false;
   const int NW = (dm.maxcon + 63) / 64;
-  T* dinv = w.tmp();          // quad()'s scratch, dead until the line search
+  T* dinv = (T*)w.tmp();      // quad()'s scratch, dead until the line search
   int* list = (int*)w.fa();   // actuator forces, consumed by smooth_acc
   auto dof = [=](int p) { return p == NV - 1 ? 0 : p + 1; };
   auto tree_of = [=](int p) { return p == NV - 1 ? 0 : (p < A0 - 1 ? 1 + p / 6 : 1 + K + (p - (A0 - 1)) / 9); };
@@ -2382,7 +2387,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
   // substitutions: the forward pass reads dir as the running right-hand side and writes y to yv (the row list's
   // array, free now), the backward pass runs on yv and writes x to dir -- one wave barrier per pivot
   T* yv = (T*)w.fa();
-  for (int p = LANE; p < NV; p += WAVE) dir[dof(p)] = -g[dof(p)];
+  for (int p = LANE; p < NV; p += WAVE) dir[dof(p)] = (T)-g[dof(p)];
   SYNC();
   for (int k = 0; k < NV; k++) {  // L y = -g, column by column over the pivot's row set
     const int tk = tree_of(k), dk = dof(k);
@@ -2406,7 +2411,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
 }
 
 template <typename T, int NVM>
-__device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const T* g, T* dir) {
+__device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const double* g, T* dir) {
   const int j = LANE;
   const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
   T col[NVM];
@@ -2437,7 +2442,7 @@ __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const 
   }
   // forward: L y = -g ; y_k is formed on lane k and broadcast (v_readlane for fp32; ds_bpermute for
   // fp64, whose split 64-bit v_readlane miscompiles in the fully unrolled fixed-size kernel)
-  T acc = j < nv ? -g[j] : T(0);
+  T acc = j < nv ? (T)-g[j] : T(0);
   T y = T(0);
 #pragma unroll
   for (int k = 0; k < NVM; k++) {
@@ -2471,9 +2476,11 @@ __device__ __forceinline__ T edge_val(const T* x3, T mu, int e) {
 
 // contact-frame products B x for every contact: one lane per (contact, frame row), the <= 9 + 9 columns
 // unrolled with unconditional loads (x[o + j] stays inside the nv vector for every tree; columns past the
-// contact's own are selected away, never multiplied), result in the record's slot .. slot + 2
-template <typename T, typename DIM>
-__device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& w, const T* x, int ncon, int slot) {
+// contact's own are selected away, never multiplied), accumulated in O and stored as O at the record's slot
+// (O = T for the velocity products of the rows' reference accelerations; O = double for the Newton iterate's
+// products JA / JD, whose float-by-float terms are exact in double)
+template <typename O, typename T, typename DIM, typename X>
+__device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& w, const X* x, int ncon, int slot) {
   const DIM dm(M.dm);
   for (int e = LANE; e < 3 * ncon; e += WAVE) {
     const int c = e / 3, r = e - 3 * c;
@@ -2483,91 +2490,111 @@ __device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& 
     const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
     const T* J = cr + CR_J + r * CJ;
     const T* Jb = J + nda;
-    T s = 0;
+    O s = 0;
 #pragma unroll
     for (int j = 0; j < 9; j++) {
-      const T ja = J[j], xa = x[oa + j];
-      s += (j < nda ? ja : T(0)) * xa;
+      const T ja = J[j];
+      const X xa = x[oa + j];
+      s += (j < nda ? (O)ja : O(0)) * (O)xa;
     }
 #pragma unroll
     for (int j = 0; j < 9; j++) {
-      const T jb = Jb[j], xb = x[ob + j];
-      s += (j < ndb ? jb : T(0)) * xb;
+      const T jb = Jb[j];
+      const X xb = x[ob + j];
+      s += (j < ndb ? (O)jb : O(0)) * (O)xb;
     }
-    cr[slot + r] = s;
+    ((O*)(cr + slot))[r] = s;
   }
 }
 
+// The solver's precision split (both builds): the problem data -- J, D, aref, M, qacc_smooth -- are the build's
+// reals; the iterate a, its products J a / M (a - as) / J dir / M dir, the gradient, the cost and the line
+// search are float64, so the iteration converges to the optimum of the rounded problem instead of stalling at the
+// float cost's resolution (sqrt(eps) in the argmin).  The Hessian and its Cholesky factor stay in the build's
+// precision: an approximate Newton direction only slows the convergence (iterative refinement), it does not move
+// the optimum.
+
 // constraint part of the primal cost at the current CR_JA / RR_JAR: sum of 1/2 D jar^2 over active rows
 template <typename T, typename DIM>
-__device__ __forceinline__ T rows_cost(const Ws<T, DIM>& w, int ncon, int nrow) {
-  T cst = 0;
+__device__ __forceinline__ double rows_cost(const Ws<T, DIM>& w, int ncon, int nrow) {
+  double cst = 0;
   for (int c = LANE; c < ncon; c += WAVE) {
     const T* cr = w.cr() + CR_N * c;
     const T mu = cr[CR_MU], D = cr[CR_D], bd = cr[CR_BD], kd = cr[CR_KD];
+    const double* ja = dslot(cr, CR_JA);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
-      T jar = edge_val(cr + CR_JA, mu, e) - aref;
-      if (jar < T(0)) cst += T(0.5) * D * jar * jar;
+      const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
+      const double jar = edge_val(ja, (double)mu, e) - (double)aref;
+      if (jar < 0.0) cst += 0.5 * (double)D * jar * jar;
     }
   }
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
     const T* rr = w.rr() + RR_N * r;
-    const T jar = rr[RR_JAR];
-    if (ri[2] == 0 || jar < T(0)) cst += T(0.5) * rr[RR_D] * jar * jar;
+    const double jar = *dslot(rr, RR_JAR);
+    if (ri[2] == 0 || jar < 0.0) cst += 0.5 * (double)rr[RR_D] * jar * jar;
   }
   return wave_sum(cst);
 }
 
 // evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
-template <typename T, typename DIM>
-__device__ __forceinline__ T rows_eval(const Model<T>& M, const Ws<T, DIM>& w, const T* x, int ncon, int nrow) {
-  contact_jx(M, w, x, ncon, CR_JA);
+template <typename T, typename DIM, typename X>
+__device__ __forceinline__ double rows_eval(const Model<T>& M, const Ws<T, DIM>& w, const X* x, int ncon, int nrow) {
+  contact_jx<double>(M, w, x, ncon, CR_JA);
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
     T* rr = w.rr() + RR_N * r;
-    rr[RR_JAR] = rr[RR_C0] * x[ri[0]] + (ri[1] >= 0 ? rr[RR_C1] * x[ri[1]] : T(0)) - rr[RR_AREF];
+    *dslot(rr, RR_JAR) = (double)rr[RR_C0] * (double)x[ri[0]] +
+                         (ri[1] >= 0 ? (double)rr[RR_C1] * (double)x[ri[1]] : 0.0) - (double)rr[RR_AREF];
   }
   SYNC();
   return rows_cost(w, ncon, nrow);
 }
 
-// f3 (per contact, stored in CR_F[0..2]) = D * sum_active jar_e c_e ; used for gradient / forces
+// f3 (per contact, float64 in CR_F3) = D * sum_active jar_e c_e, the frame force of the gradient; the edge forces
+// -D jar_e (active edges) in CR_F
 template <typename T, typename DIM>
 __device__ __forceinline__ void contact_f3(const Ws<T, DIM>& w, int ncon) {
   for (int c = LANE; c < ncon; c += WAVE) {
     T* cr = w.cr() + CR_N * c;
-    T mu = cr[CR_MU], D = cr[CR_D];
-    T f0 = 0, f1 = 0, f2 = 0;
+    const T mu = cr[CR_MU], D = cr[CR_D];
+    const double* ja = dslot(cr, CR_JA);
+    double f0 = 0, f1 = 0, f2 = 0;
+    T fe[4];
+#pragma unroll
     for (int e = 0; e < 4; e++) {
-      T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
-      T jar = edge_val(cr + CR_JA, mu, e) - aref;
-      if (jar < T(0)) {
-        T s = D * jar;
+      const T aref = -cr[CR_BD] * edge_val(cr + CR_VEL, mu, e) - cr[CR_KD];
+      const double jar = edge_val(ja, (double)mu, e) - (double)aref;
+      fe[e] = T(0);
+      if (jar < 0.0) {
+        const double s = (double)D * jar;
         f0 += s;
         if (e < 2)
-          f1 += ((e & 1) ? -mu : mu) * s;
+          f1 += ((e & 1) ? -(double)mu : (double)mu) * s;
         else
-          f2 += ((e & 1) ? -mu : mu) * s;
+          f2 += ((e & 1) ? -(double)mu : (double)mu) * s;
+        fe[e] = (T)(-s);
       }
-      cr[CR_F + e] = jar < T(0) ? -D * jar : T(0);
     }
-    cr[CR_JD + 0] = f0;  // temporarily hold f3 in the JD slots (overwritten by the line search)
-    cr[CR_JD + 1] = f1;
-    cr[CR_JD + 2] = f2;
+    double* f3 = dslot(cr, CR_F3);
+    f3[0] = f0;
+    f3[1] = f1;
+    f3[2] = f2;
+#pragma unroll
+    for (int e = 0; e < 4; e++) cr[CR_F + e] = fe[e];
   }
 }
 
-// out_i = sum over rows of J_ri * (D jar)_r for active rows  (constraint part of the gradient)
-template <typename T, typename DIM>
-__device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, T* out, bool add) {
+// out_i = sum over rows of J_ri * (D jar)_r for active rows  (constraint part of the gradient), accumulated in
+// float64 and stored as O (double: the gradient; T: the constraint force qfrc_constraint)
+template <typename T, typename DIM, typename O>
+__device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, O* out, bool add) {
   const DIM dm(M.dm);
   for (int i = LANE; i < dm.nv; i += WAVE) {
     int t = dof_tree(dm, i);
     int jl = i - tree_dof(dm, t);
-    T s = 0;
+    double s = 0;
     const int nh = DIM::MAXC == WAVE ? 1 : (dm.maxcon + WAVE - 1) / WAVE;
     for (int h = 0; h < nh; h++) {
     uint64_t mk = w.tmask()[h * dm.ntree + t];
@@ -2579,19 +2606,20 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& 
       int nda = (ci[3] >> 20) & 15;
       int col = ci[1] == t ? jl : nda + jl;
       const T* J = cr + CR_J;
-      s += J[col] * cr[CR_JD] + J[CJ + col] * cr[CR_JD + 1] + J[2 * CJ + col] * cr[CR_JD + 2];
+      const double* f3 = dslot(cr, CR_F3);
+      s += (double)J[col] * f3[0] + (double)J[CJ + col] * f3[1] + (double)J[2 * CJ + col] * f3[2];
     }
     }
     for (int r = 0; r < nrow; r++) {
       const int* ri = w.ri() + 4 * r;
       const T* rr = w.rr() + RR_N * r;
-      T jar = rr[RR_JAR];
-      if (!(ri[2] == 0 || jar < T(0))) continue;
-      T fr = rr[RR_D] * jar;
-      if (ri[0] == i) s += rr[RR_C0] * fr;
-      if (ri[1] == i) s += rr[RR_C1] * fr;
+      const double jar = *dslot(rr, RR_JAR);
+      if (!(ri[2] == 0 || jar < 0.0)) continue;
+      const double fr = (double)rr[RR_D] * jar;
+      if (ri[0] == i) s += (double)rr[RR_C0] * fr;
+      if (ri[1] == i) s += (double)rr[RR_C1] * fr;
     }
-    out[i] = add ? out[i] + s : s;
+    out[i] = add ? (O)((double)out[i] + s) : (O)s;
   }
 }
 
@@ -2600,35 +2628,35 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   const DIM dm(M.dm);
   const int nv = dm.nv;
   const int ncon = w.misc()[MISC_NCON], nrow = w.misc()[MISC_NROW];
-  T* a = w.a();
-  T* as = w.as();
-  T* g = w.g();
+  double* a = w.a();
+  const T* as = w.as();
+  double* g = w.g();
   T* dir = w.dir();
-  T* Ma = w.Ma();
-  T* tmp = w.tmp();
+  double* Ma = w.Ma();
+  double* tmp = w.tmp();
   T* H = w.H();
-  const T scale = T(1) / (M.meaninertia[arena] * T(nv > 1 ? nv : 1));
-  const T tol = (T)M.solver_tol;
+  const double scale = 1.0 / ((double)M.meaninertia[arena] * (double)(nv > 1 ? nv : 1));
+  const double tol = M.solver_tol;
   // quadratic part helper: returns 1/2 (x-as)' M (x-as), leaves M(x-as) in Ma
-  auto quad = [&](const T* x) -> T {
-    for (int i = LANE; i < nv; i += WAVE) tmp[i] = x[i] - as[i];
+  auto quad = [&](const double* x) -> double {
+    for (int i = LANE; i < nv; i += WAVE) tmp[i] = x[i] - (double)as[i];
     SYNC();
     mmul(M, w, arena, tmp, Ma);
     SYNC();
-    T s = 0;
-    for (int i = LANE; i < nv; i += WAVE) s += T(0.5) * tmp[i] * Ma[i];
+    double s = 0;
+    for (int i = LANE; i < nv; i += WAVE) s += 0.5 * tmp[i] * Ma[i];
     return wave_sum(s);
   };
-  // warmstart: the cheaper of qacc_warmstart and qacc_smooth.  The smooth candidate is evaluated first, so
-  // in the common case (the warmstart wins) the row products and M(a - as) left behind are already those
-  // of the chosen start and need no third evaluation
-  const T c_sm = quad(as) + rows_eval(M, w, as, ncon, nrow);
+  // warmstart: the cheaper of qacc_warmstart and qacc_smooth.  The smooth candidate is evaluated first (its
+  // quadratic part is zero), so in the common case (the warmstart wins) the row products and M(a - as) left
+  // behind are already those of the chosen start and need no third evaluation
+  const double c_sm = rows_eval(M, w, as, ncon, nrow);
   SYNC();
-  T qc = quad(a);
-  T cost = qc + rows_eval(M, w, a, ncon, nrow);
+  double qc = quad(a);
+  double cost = qc + rows_eval(M, w, a, ncon, nrow);
   SYNC();
   if (!(cost < c_sm)) {
-    for (int i = LANE; i < nv; i += WAVE) a[i] = as[i];
+    for (int i = LANE; i < nv; i += WAVE) a[i] = (double)as[i];
     SYNC();
     qc = quad(a);
     cost = qc + rows_eval(M, w, a, ncon, nrow);
@@ -2644,7 +2672,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SYNC();
     gather_JtF(M, w, ncon, nrow, g, false);
     SYNC();
-    T gn = 0;
+    double gn = 0;
     for (int i = LANE; i < nv; i += WAVE) {
       g[i] += Ma[i];
       gn += g[i] * g[i];
@@ -2717,7 +2745,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     for (int r = LANE; r < nrow; r += WAVE) {
       const int* ri = w.ri() + 4 * r;
       const T* rr = w.rr() + RR_N * r;
-      if (!(ri[2] == 0 || rr[RR_JAR] < T(0))) continue;
+      if (!(ri[2] == 0 || *dslot(rr, RR_JAR) < 0.0)) continue;
       const T D = rr[RR_D];
       const int d0 = ri[0], d1 = ri[1];
       atomicAdd(H + d0 * nv + d0, D * rr[RR_C0] * rr[RR_C0]);
@@ -2765,7 +2793,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       }
       PMARK(PH_NCHOL);
       // dir = -H^-1 g  (column-oriented substitutions)
-      for (int i = LANE; i < nv; i += WAVE) dir[i] = -g[i];
+      for (int i = LANE; i < nv; i += WAVE) dir[i] = (T)-g[i];
       SYNC();
       for (int k = 0; k < nv; k++) {
         T xk = dir[k] / H[k * nv + k];
@@ -2785,18 +2813,19 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     PMARK(PH_NSOLVE);
     // exact line search along dir (segment walking over the breakpoints of the inequality rows)
     // Jd per contact (frame components) and per generic row
-    contact_jx(M, w, dir, ncon, CR_JD);
+    contact_jx<double>(M, w, dir, ncon, CR_JD);
     for (int r = LANE; r < nrow; r += WAVE) {
       const int* ri = w.ri() + 4 * r;
       T* rr = w.rr() + RR_N * r;
-      rr[RR_JD] = rr[RR_C0] * dir[ri[0]] + (ri[1] >= 0 ? rr[RR_C1] * dir[ri[1]] : T(0));
+      *dslot(rr, RR_JD) = (double)rr[RR_C0] * (double)dir[ri[0]] +
+                          (ri[1] >= 0 ? (double)rr[RR_C1] * (double)dir[ri[1]] : 0.0);
     }
     mmul(M, w, arena, dir, tmp);
     SYNC();
-    T dMd = 0, dMa = 0;
+    double dMd = 0, dMa = 0;
     for (int i = LANE; i < nv; i += WAVE) {
-      dMd += dir[i] * tmp[i];
-      dMa += dir[i] * Ma[i];
+      dMd += (double)dir[i] * tmp[i];
+      dMa += (double)dir[i] * Ma[i];
     }
     dMd = wave_sum(dMd);
     dMa = wave_sum(dMa);
@@ -2804,8 +2833,10 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     // one generic row per lane (nrow <= 64) held in registers; padding slots carry jd = 0, D = 0 and contribute
     // nothing
     constexpr int NHC = DIM::MAXC / WAVE;
-    T ejar[4 * NHC], ejd[4 * NHC], ete[4 * NHC], eD[NHC];
-    T gjar = T(0), gjd = T(0), gte = T(0), gD = T(0);
+    double ejar[4 * NHC], ejd[4 * NHC], ete[4 * NHC];
+    T eD[NHC];
+    double gjar = 0, gjd = 0, gte = 0;
+    T gD = T(0);
     bool geq = false;
 #pragma unroll
     for (int h = 0; h < NHC; h++) {
@@ -2813,69 +2844,72 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       if (LANE + WAVE * h < ncon) {
         const T* cr = w.cr() + CR_N * (LANE + WAVE * h);
         const T mu = cr[CR_MU], bd = cr[CR_BD], kd = cr[CR_KD];
+        const double* ja = dslot(cr, CR_JA);
+        const double* jd = dslot(cr, CR_JD);
         eD[h] = cr[CR_D];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
-          ejar[4 * h + e] = edge_val(cr + CR_JA, mu, e) - aref;
-          ejd[4 * h + e] = edge_val(cr + CR_JD, mu, e);
-          ete[4 * h + e] = ejd[4 * h + e] != T(0) ? -ejar[4 * h + e] / ejd[4 * h + e] : T(0);
+          ejar[4 * h + e] = edge_val(ja, (double)mu, e) - (double)aref;
+          ejd[4 * h + e] = edge_val(jd, (double)mu, e);
+          ete[4 * h + e] = ejd[4 * h + e] != 0.0 ? -ejar[4 * h + e] / ejd[4 * h + e] : 0.0;
         }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-          ejar[4 * h + e] = T(1);
-          ejd[4 * h + e] = T(0);
-          ete[4 * h + e] = T(0);
+          ejar[4 * h + e] = 1.0;
+          ejd[4 * h + e] = 0.0;
+          ete[4 * h + e] = 0.0;
         }
       }
     }
     if (LANE < nrow) {
       const T* rr = w.rr() + RR_N * LANE;
       geq = w.ri()[4 * LANE + 2] == 0;
-      gjar = rr[RR_JAR];
-      gjd = rr[RR_JD];
+      gjar = *dslot(rr, RR_JAR);
+      gjd = *dslot(rr, RR_JD);
       gD = rr[RR_D];
-      gte = gjd != T(0) ? -gjar / gjd : T(0);
+      gte = gjd != 0.0 ? -gjar / gjd : 0.0;
     }
-    T alpha = 0;
+    double alpha = 0;
     for (int ls = 0; ls < 4 * (4 * ncon + nrow) + 4; ls++) {
-      T c0 = 0, c1 = 0, tn = T(3.0e38);
+      double c0 = 0, c1 = 0, tn = 1.0e300;
 #pragma unroll
       for (int e = 0; e < 4 * NHC; e++) {
-        const T jar = ejar[e], jd = ejd[e], te = ete[e];
+        const double jar = ejar[e], jd = ejd[e], te = ete[e];
         bool act;
-        if (jd != T(0)) {
-          act = jd < T(0) ? te <= alpha : alpha < te;
+        if (jd != 0.0) {
+          act = jd < 0.0 ? te <= alpha : alpha < te;
           if (te > alpha && te < tn) tn = te;
         } else {
-          act = jar < T(0);
+          act = jar < 0.0;
         }
         if (act) {
-          c0 += eD[e / 4] * (jar + alpha * jd) * jd;
-          c1 += eD[e / 4] * jd * jd;
+          const double De = (double)eD[e / 4];
+          c0 += De * (jar + alpha * jd) * jd;
+          c1 += De * jd * jd;
         }
       }
       {
         bool act;
         if (geq) {
           act = true;
-        } else if (gjd != T(0)) {
-          act = gjd < T(0) ? gte <= alpha : alpha < gte;
+        } else if (gjd != 0.0) {
+          act = gjd < 0.0 ? gte <= alpha : alpha < gte;
           if (gte > alpha && gte < tn) tn = gte;
         } else {
-          act = gjar < T(0);
+          act = gjar < 0.0;
         }
         if (act) {
-          c0 += gD * (gjar + alpha * gjd) * gjd;
-          c1 += gD * gjd * gjd;
+          c0 += (double)gD * (gjar + alpha * gjd) * gjd;
+          c1 += (double)gD * gjd * gjd;
         }
       }
       c0 = wave_sum(c0) + dMa + alpha * dMd;
       c1 = wave_sum(c1) + dMd;
       tn = wave_min(tn);
-      if (c0 >= T(0)) break;
-      T astar = alpha - c0 / c1;
+      if (c0 >= 0.0) break;
+      const double astar = alpha - c0 / c1;
       if (astar <= tn) {
         alpha = astar;
         break;
@@ -2885,29 +2919,25 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     // step: a, M (a - as) and the row products all move along dir (MuJoCo's Newton updates Jaref and Ma
     // the same way instead of recomputing them); the quadratic part of the cost follows exactly
     for (int i = LANE; i < nv; i += WAVE) {
-      a[i] += alpha * dir[i];
+      a[i] += alpha * (double)dir[i];
       Ma[i] += alpha * tmp[i];
     }
     for (int e = LANE; e < 3 * ncon; e += WAVE) {
-      T* cr = w.cr() + CR_N * (e / 3) + e % 3;
-      cr[CR_JA] += alpha * cr[CR_JD];
+      T* cr = w.cr() + CR_N * (e / 3);
+      dslot(cr, CR_JA)[e % 3] += alpha * dslot(cr, CR_JD)[e % 3];
     }
     for (int r = LANE; r < nrow; r += WAVE) {
       T* rr = w.rr() + RR_N * r;
-      rr[RR_JAR] += alpha * rr[RR_JD];
+      *dslot(rr, RR_JAR) += alpha * *dslot(rr, RR_JD);
     }
     SYNC();
-    qc += alpha * dMa + T(0.5) * alpha * alpha * dMd;
-    T newcost = qc + rows_cost(w, ncon, nrow);
+    qc += alpha * dMa + 0.5 * alpha * alpha * dMd;
+    const double newcost = qc + rows_cost(w, ncon, nrow);
     SYNC();
     PMARK(PH_NLS);
-    T improvement = scale * (cost - newcost);
-    // fp32: the cost itself carries rounding noise of a few ulp of its magnitude; an "improvement" inside
-    // that band is not progress (without this a stiff arena can spin to the iteration cap, and one such
-    // arena sets the whole launch's duration)
-    const T noise = (sizeof(T) == 4 && !(M.dbg_flags & 2)) ? T(4.8e-7) * fabs(scale * newcost) : T(0);
+    const double improvement = scale * (cost - newcost);
     cost = newcost;
-    if (improvement < tol || improvement <= noise) {
+    if (improvement < tol) {
       it++;
       break;
     }
@@ -2923,7 +2953,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
     T* rr = w.rr() + RR_N * r;
-    rr[RR_F] = (ri[2] == 0 || rr[RR_JAR] < T(0)) ? -rr[RR_D] * rr[RR_JAR] : T(0);
+    const double jar = *dslot(rr, RR_JAR);
+    rr[RR_F] = (ri[2] == 0 || jar < 0.0) ? (T)(-(double)rr[RR_D] * jar) : T(0);
   }
   SYNC();
   PMARK(PH_NFINAL);
@@ -3006,36 +3037,40 @@ __device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T, DIM>& 
   SYNC();
 }
 
+#ifndef FM_INT_F64
+#define FM_INT_F64 0  // experiment: the implicitfast acceleration solve in float64 for the fp32 build
+#endif
 template <typename T, typename DIM>
 __device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T, DIM>& w, int arena, bool actuation) {
+  using IT = std::conditional_t<FM_INT_F64 != 0, double, T>;
   const DIM dm(M.dm);
   const int K = dm.K, nv = dm.nv;
-  const T dt = M.dt;
+  const IT dt = (IT)M.dt;
   T* q = w.q();
   T* v = w.v();
-  T* acc = w.tmp();
+  IT* acc = (IT*)w.tmp();  // the solver's float64 scratch
   int a0 = 1 + 6 * K;
   // belt: M + dt*(kv + damping); cubes: M
   if (LANE == 0) {
-    T mb = M.belt_mass + dt * M.belt_damp + (actuation ? dt * M.belt_kv : T(0));
-    acc[0] = (w.fs()[0] + w.fc()[0]) / mb;
+    IT mb = (IT)M.belt_mass + dt * (IT)M.belt_damp + (actuation ? dt * (IT)M.belt_kv : IT(0));
+    acc[0] = ((IT)w.fs()[0] + (IT)w.fc()[0]) / mb;
   }
-  for (int i = 1 + LANE; i < a0; i += WAVE) acc[i] = (w.fs()[i] + w.fc()[i]) / Mdiag(M, w, i);
+  for (int i = 1 + LANE; i < a0; i += WAVE) acc[i] = ((IT)w.fs()[i] + (IT)w.fc()[i]) / (IT)Mdiag(M, w, i);
   if (LANE < dm.A) {
     const T* Mb = w.Marm() + 81 * LANE;
-    T Lp[45], x[9];
+    IT Lp[45], x[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) {
 #pragma unroll
-      for (int j = 0; j <= i; j++) Lp[P9(i, j)] = Mb[9 * i + j];
-      x[i] = w.fs()[a0 + 9 * LANE + i] + w.fc()[a0 + 9 * LANE + i];
+      for (int j = 0; j <= i; j++) Lp[P9(i, j)] = (IT)Mb[9 * i + j];
+      x[i] = (IT)w.fs()[a0 + 9 * LANE + i] + (IT)w.fc()[a0 + 9 * LANE + i];
     }
     if (actuation) {
 #pragma unroll
-      for (int j = 0; j < 7; j++) Lp[P9(j, j)] += dt * T(200);
+      for (int j = 0; j < 7; j++) Lp[P9(j, j)] += dt * IT(200);
       T fg = w.aforce()[1 + 8 * LANE + 7];
       if (fg > T(-100) && fg < T(100)) {
-        T d = dt * T(10) * T(0.25);
+        IT d = dt * IT(10) * IT(0.25);
         Lp[P9(7, 7)] += d;
         Lp[P9(8, 8)] += d;
         Lp[P9(8, 7)] += d;
@@ -3377,7 +3412,7 @@ __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w
 // phase-local H region as scratch (free outside a substep's stage / solve).  Not inlined (it runs a few times
 // per env-step): every pointer it receives is global or LDS -- none into a caller's private frame, which a
 // callee could only reach through the flat scratch aperture.
-__device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const double* ctrlrange_d, int A, int K,
+__device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const double* ctrlrange_d, IkTiming tm, int A, int K,
                                             const double* qd, const double* vd, int32_t* ti, double* td,
                                             int int_base, int dbl_base, double* scr, double* prop) {
   // scr per arm (24): grip 3 | tpos 3 | tquat 4 | need | close | pad 2 | q 7 | pad 3
@@ -3401,7 +3436,7 @@ __device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const doub
       double* sc = scr + 24 * i;
       int cl = 0;
       double g[3] = {sc[0], sc[1], sc[2]}, tp[3] = {0, 0, 0}, tq[4] = {1, 0, 0, 0};
-      sc[10] = ik_plan(A, i, p, ti, n_in, qd, vd, K, g, arm_base_w + 12 * i, tp, tq, &cl);
+      sc[10] = ik_plan(A, i, p, ti, n_in, qd, vd, K, g, arm_base_w + 12 * i, tm, tp, tq, &cl);
       for (int k = 0; k < 3; k++) sc[3 + k] = tp[k];
       for (int k = 0; k < 4; k++) sc[6 + k] = tq[k];
       sc[11] = cl;
@@ -3439,7 +3474,7 @@ __device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const doub
 template <typename T, typename DIM>
 __device__ __forceinline__ void ik_compose(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td, double* prop) {
   const DIM dm(M.dm);
-  ik_compose_raw(M.arm_base_w, M.ctrlrange_d, dm.A, dm.K, w.qd(), w.vd(), ti, td, 0, 0, (double*)w.H(), prop);
+  ik_compose_raw(M.arm_base_w, M.ctrlrange_d, M.ik_time, dm.A, dm.K, w.qd(), w.vd(), ti, td, 0, 0, (double*)w.H(), prop);
 }
 
 // IKTogglingEnv._process_observation (environments.py:560-577): fresh proposals, kept for the next step's
@@ -3510,7 +3545,7 @@ __device__ __forceinline__ void arena_reset(const Model<T>& M, const Ws<T, DIM>&
   for (int i = LANE; i < dm.nq; i += WAVE) q[i] = 0.0;
   for (int i = LANE; i < dm.nv; i += WAVE) {
     v[i] = 0.0;
-    w.a()[i] = T(0);
+    w.a()[i] = 0.0;
   }
   SYNC();
   if (LANE == 0) task_reset<T, DIM>(M, q, v, ti, td, w.ctrl());
@@ -3534,7 +3569,7 @@ __device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S
   double* ph = S.phys + (size_t)arena * dm.phys_stride;
   for (int i = LANE; i < dm.nq; i += WAVE) ph[i] = w.qd()[i];
   for (int i = LANE; i < dm.nv; i += WAVE) ph[dm.nq + i] = w.vd()[i];
-  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + 2 * dm.nv + i] = (double)w.a()[i];
+  for (int i = LANE; i < dm.nv; i += WAVE) ph[2 * dm.nq + 2 * dm.nv + i] = w.a()[i];
   double* db = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < dm.nu; u += WAVE) db[u] = w.ctrl()[u];
 }
@@ -3654,7 +3689,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   init_arena(M, w, arena);
   // warmstart
   const double* ph = S.phys + (size_t)arena * dm.phys_stride;
-  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = (T)ph[2 * dm.nq + 2 * dm.nv + i];
+  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
   SYNC();
   // stage (mj_step1) at the state of the last mj_step1 (pre-teleport), then integrate the current state
   load_state(M, S, w, arena, true);
@@ -3770,7 +3805,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     for (int i = LANE; i < dm.nq; i += WAVE) w.qd()[i] = 0.0;
     for (int i = LANE; i < dm.nv; i += WAVE) {
       w.vd()[i] = 0.0;
-      w.a()[i] = T(0);
+      w.a()[i] = 0.0;
     }
     SYNC();
     if (LANE == 0) {
@@ -3826,17 +3861,39 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
   const double* ph = S.phys + (size_t)arena * dm.phys_stride;
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
   for (int u = LANE; u < dm.nu; u += WAVE) w.ctrl()[u] = dsrc[u];
-  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = (T)ph[2 * dm.nq + 2 * dm.nv + i];
+  for (int i = LANE; i < dm.nv; i += WAVE) w.a()[i] = ph[2 * dm.nq + 2 * dm.nv + i];
   init_arena(M, w, arena);
   SYNC();
   load_state(M, S, w, arena, true);
   SYNC();
   stage(M, w, arena, ctr);
   smooth_acc(M, w, arena, actuated != 0);
-  if (w.misc()[MISC_NCON] + w.misc()[MISC_NROW] > 0) newton(M, w, arena, ctr);
-  SYNC();
   const int A = dm.A, nv = dm.nv;
   int ncon = w.misc()[MISC_NCON], nrow = w.misc()[MISC_NROW];
+  const double zs = zshift<T>();
+  // the contacts' geometry first: the solver reuses those record slots for its float64 row products
+  {
+    double* oc = out + 2 + 81 * A + 4 * nv + 3 * A + 60 * A + 27 * A;
+    for (int c = LANE; c < 64; c += WAVE) {
+      double* r = oc + 17 * c;
+      if (c < ncon) {
+        const int* ci = w.ci() + 4 * c;
+        const T* cr = w.cr() + CR_N * c;
+        r[0] = M.geom_i[4 * (ci[0] & 4095)];
+        r[1] = M.geom_i[4 * ((ci[0] >> 12) & 4095)];
+        r[2] = cr[CR_DIST];
+        for (int k = 0; k < 3; k++) r[3 + k] = (double)cr[CR_POS + k] + (k == 2 ? zs : 0.0);
+        for (int k = 0; k < 9; k++) r[6 + k] = cr[CR_FR + k];
+        r[15] = cr[CR_MU];
+        r[16] = cr[CR_D];
+      } else {
+        for (int k = 0; k < 17; k++) r[k] = 0;
+      }
+    }
+  }
+  SYNC();
+  if (ncon + nrow > 0) newton(M, w, arena, ctr);
+  SYNC();
   double* o = out;
   if (LANE == 0) {
     o[0] = ncon;
@@ -3853,7 +3910,6 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
   }
   o += 4 * nv;
   // positions back in the world frame (zshift)
-  const double zs = zshift<T>();
   for (int i = LANE; i < 3 * A; i += WAVE) o[i] = (double)w.site()[i] + (i % 3 == 2 ? zs : 0.0);
   o += 3 * A;
   for (int i = LANE; i < 30 * A; i += WAVE) {
@@ -3863,22 +3919,6 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
   o += 60 * A;
   for (int i = LANE; i < 27 * A; i += WAVE) o[i] = (double)w.dax()[i];
   o += 27 * A;
-  for (int c = LANE; c < 64; c += WAVE) {
-    double* r = o + 17 * c;
-    if (c < ncon) {
-      const int* ci = w.ci() + 4 * c;
-      const T* cr = w.cr() + CR_N * c;
-      r[0] = M.geom_i[4 * (ci[0] & 4095)];
-      r[1] = M.geom_i[4 * ((ci[0] >> 12) & 4095)];
-      r[2] = cr[CR_DIST];
-      for (int k = 0; k < 3; k++) r[3 + k] = (double)cr[CR_POS + k] + (k == 2 ? zs : 0.0);
-      for (int k = 0; k < 9; k++) r[6 + k] = cr[CR_FR + k];
-      r[15] = cr[CR_MU];
-      r[16] = cr[CR_D];
-    } else {
-      for (int k = 0; k < 17; k++) r[k] = 0;
-    }
-  }
   o += 17 * 64;
   for (int r = LANE; r < 20 * A; r += WAVE) {
     double* x = o + 6 * r;

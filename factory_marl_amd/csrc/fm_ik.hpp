@@ -304,7 +304,7 @@ __device__ __noinline__ int ik_solve(const double* base, double* q, const double
 // Returns 1 when an IK solve for (tp, tq) follows, 0 when act() returned idle_ctrl().
 __device__ __forceinline__ int ik_plan(int A, int i, IkArm p, const int32_t* in_scene, int n_in, const double* qd,
                                        const double* vd, int K, const double* grip, const double* base,
-                                       double* tp, double* tq, int* close) {
+                                       const IkTiming& tm, double* tp, double* tq, int* close) {
   int32_t* st = p.s;  // state, counter, target, ignore[A]
   const int qa = 1 + 7 * K + 9 * i;
   // select_target_object (ik_policy.py:92-118): candidates = in-scene cubes not in ignore_objects.values()
@@ -374,7 +374,7 @@ __device__ __forceinline__ int ik_plan(int A, int i, IkArm p, const int32_t* in_
       if (near) set_state(IK_GRASP_CLOSE);
       break;
     case IK_GRASP_CLOSE:
-      if (near && counter > 10) {
+      if (near && counter > tm.grasp_wait) {
         for (int k = 0; k < 3; k++) ms[k] = grip[k];
         set_state(IK_POST_GRASP);
       } else if (!near) {
@@ -396,10 +396,10 @@ __device__ __forceinline__ int ik_plan(int A, int i, IkArm p, const int32_t* in_
         set_state(IK_RELEASE);
       break;
     default:  // RELEASE
-      if (counter > 5) set_state(IK_IDLE);
+      if (counter > tm.release_wait) set_state(IK_IDLE);
       break;
   }
-  const double t = (double)counter / 10;
+  const double t = (double)counter / tm.move_steps;
   bool comp = false;
   int cl = 0;
   const double defq[4] = {0, 0, 1, 0};
@@ -438,14 +438,13 @@ __device__ __forceinline__ int ik_plan(int A, int i, IkArm p, const int32_t* in_
       break;
   }
   counter++;
-  if (counter > 30) {
+  if (counter > tm.timeout_steps) {
     idle();
     return 0;
   }
   if (comp) {
-    const double pc = 0.2 * 0.1 * 15.0;  // env.pt_time * env.dt * 15.0
-    tp[0] += ov[0] * pc;
-    tp[1] += ov[1] * pc;
+    tp[0] += ov[0] * tm.pt_comp;  // env.pt_time * env.dt * 15.0
+    tp[1] += ov[1] * tm.pt_comp;
   }
   for (int k = 0; k < 4; k++) tq[k] = quat[k];
   st[0] = state;

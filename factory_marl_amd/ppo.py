@@ -101,7 +101,8 @@ class ActorCriticPolicy(nn.Module):
         ent = 0.5 + 0.5 * math.log(2 * math.pi) + self.log_std
         return logp.sum(-1), ent.expand_as(head).sum(-1)
 
-    def _sample(self, head, deterministic):
+    def _sample(self, head, deterministic, generator=None):
+        """`generator`: the sampling stream (PPO keeps one per rank); None = torch's global RNG"""
         if self.discrete:
             outs, o = [], 0
             for n in self.nvec:
@@ -110,16 +111,17 @@ class ActorCriticPolicy(nn.Module):
                 if deterministic:
                     outs.append(logits.argmax(-1))
                 else:
-                    outs.append(torch.multinomial(torch.softmax(logits, -1), 1).squeeze(1))
+                    outs.append(torch.multinomial(torch.softmax(logits, -1), 1, generator=generator).squeeze(1))
             return torch.stack(outs, 1).to(torch.float32)
         if deterministic:
             return head
-        return head + self.log_std.exp() * torch.randn_like(head)
+        noise = torch.randn(head.shape, device=head.device, dtype=head.dtype, generator=generator)
+        return head + self.log_std.exp() * noise
 
     # ------------------------------------------------------------------ SB3 API
-    def forward(self, obs, deterministic=False):
+    def forward(self, obs, deterministic=False, generator=None):
         head, values = self._dist_params(obs)
-        actions = self._sample(head, deterministic)
+        actions = self._sample(head, deterministic, generator)
         logp, _ = self._log_prob_entropy(head, actions)
         return actions, values, logp
 
@@ -132,9 +134,9 @@ class ActorCriticPolicy(nn.Module):
         return self.value_net(self.mlp_extractor.value_net(obs)).squeeze(-1)
 
     @torch.no_grad()
-    def predict(self, obs, deterministic=True):
+    def predict(self, obs, deterministic=True, generator=None):
         head, _ = self._dist_params(obs)
-        return self._sample(head, deterministic)
+        return self._sample(head, deterministic, generator)
 
     @classmethod
     def for_env(cls, env, net_arch=(128, 128), **kw):
@@ -185,8 +187,14 @@ class PPO:
                        gamma=gamma, gae_lambda=gae_lambda, clip_range=clip_range, ent_coef=ent_coef, vf_coef=vf_coef,
                        max_grad_norm=max_grad_norm, normalize_advantage=normalize_advantage, seed=seed,
                        world_size=self.world, net_arch=list(pk["net_arch"]))
+        # per-rank streams: minibatch permutations, and the rollout's action sampling -- every rank starts from the
+        # same broadcast weights (and often identical arenas), so a shared seed would make the ranks' rollouts
+        # bit-identical and shrink the effective batch by the world size
+        rank = self.dist.get_rank() if self.dist else 0
         self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(seed + 1000 * (self.dist.get_rank() if self.dist else 0))
+        self.gen.manual_seed(seed + 1000 * rank)
+        self.sample_gen = torch.Generator(device=self.device)
+        self.sample_gen.manual_seed(seed + 7919 * (rank + 1))
         self.num_timesteps = 0
         self._last_obs = None
         self._last_starts = None
@@ -198,7 +206,8 @@ class PPO:
         env, pol, T, N = self.env, self.policy, self.hp["n_steps"], self.env.num_envs
         dev = self.device
         if self._last_obs is None:
-            self._last_obs = env.reset().clone()
+            env.reset()
+            self._last_obs = env.obs.clone()
             self._last_starts = torch.ones(N, device=dev)
         A = pol.action_dim
         buf = dict(obs=torch.empty(T, N, env.obs_dim, device=dev), actions=torch.empty(T, N, A, device=dev),
@@ -208,7 +217,7 @@ class PPO:
         ep_n = torch.zeros((), dtype=torch.float64, device=dev)
         for t in range(T):
             obs = self._last_obs
-            actions, values, logp = pol(obs)
+            actions, values, logp = pol(obs, generator=self.sample_gen)
             step_a = actions if pol.discrete else actions.clamp(-1.0, 1.0)
             new_obs, rew, term, trunc = env.step_tensors(step_a.contiguous())
             done = (term | trunc).to(torch.float32)

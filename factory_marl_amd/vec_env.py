@@ -5,8 +5,16 @@ Replaces ``make_vec_env(lambda: Monitor(Env(**env_kwargs)), n_envs, vec_env_cls=
 reset() / step_async() / step_wait() / step() / get_attr / set_attr / env_method / close / seed``
 surface and the same auto-reset + ``infos[i]["terminal_observation"]`` + Monitor
 ``infos[i]["episode"] = {"r", "l", "t"}`` semantics, but every arena lives in HBM and one HIP launch
-advances all of them (no worker processes, no pickled pipes).  Observations / rewards / dones are
-torch ROCm tensors; ``return_numpy=True`` gives numpy like SB3.
+advances all of them (no worker processes, no pickled pipes).
+
+As SB3: ``reset()`` / ``step()`` return numpy arrays.  ``return_numpy=False`` returns the torch ROCm tensors
+instead, and ``step_tensors()`` is the zero-copy device path the on-GPU trainer (ppo.py) uses.
+
+Construction: ``FactoryVecEnv(num_envs, env_class=..., env_kwargs=...)``, or SB3's ``VecEnv(env_fns)`` form -- a
+list of thunks returning ``factory_marl_amd.environments`` specs, which is what ``make_vec_env(...,
+vec_env_cls=FactoryVecEnv)`` passes (see environments.py).  Keyword arguments are resolved exactly as the reference
+constructors resolve them (``environments.resolve_kwargs``: required ProgressRewardEnv factors, base_reward 0.0,
+TypeError on unknown keywords).
 """
 import ctypes as C
 import time
@@ -14,8 +22,9 @@ import time
 import numpy as np
 
 from . import _lib
+from . import environments as envs
 
-# the env classes of src/environments.py (class hierarchy at environments.py:10-22)
+# the env classes of src/environments.py with a GPU env-step (class hierarchy at environments.py:10-22)
 ENV_CLASSES = {
     "FactoryManipulationEnv": _lib.FM_ENV_FACTORY,
     "AllFullRLProgressRewardEnv": _lib.FM_ENV_ALLFULLRL_PROGRESS,
@@ -25,18 +34,15 @@ ENV_CLASSES = {
     "PauseIKToggleEnv": _lib.FM_ENV_PAUSE_IK_TOGGLE,
     "BackupIKToggleEnv": _lib.FM_ENV_BACKUP_IK_TOGGLE,
 }
-TOGGLE_CLASSES = ("PauseIKToggleEnv", "BackupIKToggleEnv")
+TOGGLE_CLASSES = envs.TOGGLE_CLASSES
 
-# BaseEnv.__init__ defaults (base_env.py:15-35); ProgressRewardEnv weights of the saved runs
-# (runs/rk5rxnav.json env_kwargs)
-DEFAULT_KWARGS = dict(
-    num_arms=2, max_num_objects=10, seed=42, initial_conveyor_speed=0.1, conveyor_acceleration=0.001,
-    pt_time=0.2, force_contact_threshold=200.0, control_frequency=10, spawn_freq=1 / 10,
-    spawn_freq_increase=1.001, gripper_to_closest_cube_reward_factor=0.2,
-    closest_cube_to_bucket_reward_factor=0.4, small_action_norm_reward_factor=0.0, base_reward=0.4,
-)
-_IGNORED_KWARGS = {"render_mode", "width", "height", "camera_id", "camera_name", "default_camera_config",
-                   "max_geom", "visual_options"}
+# env attributes with a value on the GPU path (base_env.py:133-147, environments.py:276-282):
+# global scalars of the handle (fm_set_param), per-arena values of the state record, fixed at creation
+RUNTIME_PARAMS = ("pt_time", "initial_conveyor_speed", "conveyor_acceleration", "force_contact_threshold",
+                  "spawn_freq_increase", "init_spawn_freq", "gripper_to_closest_cube_reward_factor",
+                  "closest_cube_to_bucket_reward_factor", "small_action_norm_reward_factor", "base_reward")
+ARENA_SCALARS = ("play_time", "conveyor_speed")
+FIXED_ATTRS = ("num_arms", "max_num_objects", "seed", "control_frequency", "frame_skip", "dt")
 
 
 class Box:
@@ -69,20 +75,38 @@ class MultiDiscrete:
         return f"MultiDiscrete({self.nvec})"
 
 
+def _specs_from_env_fns(env_fns):
+    """SB3 VecEnv(env_fns): every thunk must build the same env (class and keywords), as SubprocVecEnv workers of
+    one make_vec_env do"""
+    specs = [fn() for fn in env_fns]
+    for s in specs:
+        if not isinstance(s, envs.EnvSpec):
+            raise TypeError("FactoryVecEnv(env_fns): the thunks must build factory_marl_amd.environments classes "
+                            f"(got {type(s).__name__})")
+    if any(s != specs[0] for s in specs[1:]):
+        raise ValueError("FactoryVecEnv(env_fns): every env of one batch must have the same class and keywords")
+    return specs[0]
+
+
 class FactoryVecEnv:
     def __init__(self, num_envs, env_class="AllFullRLProgressRewardEnv", env_kwargs=None, device=0,
-                 precision="fp32", seeds=None, return_numpy=False, max_contacts=0, solver_tolerance=0.0,
+                 precision="fp32", seeds=None, return_numpy=True, max_contacts=0, solver_tolerance=0.0,
                  solver_iterations=0):
         import torch
 
         self.torch = torch
-        kw = dict(DEFAULT_KWARGS)
-        kw.update({k: v for k, v in (env_kwargs or {}).items() if k not in _IGNORED_KWARGS})
+        if isinstance(num_envs, (list, tuple)):  # SB3 VecEnv(env_fns) (make_vec_env(..., vec_env_cls=FactoryVecEnv))
+            spec = _specs_from_env_fns(num_envs)
+            num_envs, env_class, kw = len(num_envs), spec.env_class, dict(spec.kwargs)
+        else:
+            if env_class not in ENV_CLASSES:
+                raise ValueError(f"env_class {env_class!r} not implemented on the GPU path; "
+                                 f"available: {sorted(ENV_CLASSES)}")
+            kw = envs.resolve_kwargs(env_class, env_kwargs or {})
         if env_class not in ENV_CLASSES:
-            raise ValueError(f"env_class {env_class!r} not implemented on the GPU path; "
-                             f"available: {sorted(ENV_CLASSES)}")
+            raise ValueError(f"env_class {env_class!r} not implemented on the GPU path; available: {sorted(ENV_CLASSES)}")
         self.env_class = env_class
-        self.env_kwargs = kw
+        self.progress = env_class in envs.PROGRESS_CLASSES
         L = _lib.load()
         cfg = _lib.FmConfig()
         L.fm_config_default(C.byref(cfg))
@@ -97,14 +121,22 @@ class FactoryVecEnv:
         if solver_iterations > 0:
             cfg.solver_iterations = int(solver_iterations)
         for k in ["initial_conveyor_speed", "conveyor_acceleration", "pt_time", "force_contact_threshold",
-                  "control_frequency", "spawn_freq", "spawn_freq_increase", "gripper_to_closest_cube_reward_factor",
-                  "closest_cube_to_bucket_reward_factor", "small_action_norm_reward_factor", "base_reward"]:
+                  "control_frequency", "spawn_freq", "spawn_freq_increase"]:
             setattr(cfg, k, float(kw[k]))
+        if self.progress:  # score-reward classes have no reward factors (their kernel path reads none)
+            for k in envs.PROGRESS_REQUIRED + ("base_reward",):
+                setattr(cfg, k, float(kw[k]))
         if seeds is None:
-            seeds = [int(kw["seed"])] * int(num_envs)
+            if kw["seed"] is None:
+                # BaseEnv(seed=None): build_scene and the TaskManager draw fresh entropy in every env
+                seeds = np.random.default_rng().integers(0, 2 ** 62, int(num_envs), dtype=np.uint64)
+            else:
+                seeds = [int(kw["seed"])] * int(num_envs)
         seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
         if len(seeds) != num_envs:
             raise ValueError("need one seed per arena")
+        self.seeds_used = seeds.copy()
+        self.env_kwargs = kw
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         h = C.c_void_p()
         _lib.check(L.fm_create(C.byref(cfg), self.device.index or 0,
@@ -144,6 +176,7 @@ class FactoryVecEnv:
         self._stream_bound = -1
         self.ep_score_history = [[] for _ in range(n)]
         self._t0 = [time.time()] * n
+        self._user_attrs = [dict() for _ in range(n)]
 
     # ------------------------------------------------------------------ core API
     def _bind_stream(self):
@@ -228,25 +261,125 @@ class FactoryVecEnv:
         return infos
 
     # ------------------------------------------------------------------ SB3 VecEnv helpers
+    def _indices(self, indices):
+        if indices is None:
+            return list(range(self.num_envs))
+        if isinstance(indices, int):
+            return [indices]
+        return [int(i) for i in indices]
+
+    def get_param(self, name):
+        v = C.c_double()
+        _lib.check(self._L.fm_get_param(self._h, name.encode(), C.byref(v)))
+        return float(v.value)
+
+    def _arena_field(self, name):
+        from . import state as st
+
+        A, K = self.env_kwargs["num_arms"], self.env_kwargs["max_num_objects"]
+        return st, A, K
+
     def get_attr(self, name, indices=None):
-        idx = range(self.num_envs) if indices is None else indices
+        """SB3 VecEnv.get_attr: the attribute of each env in `indices`"""
+        idx = self._indices(indices)
         if name == "ep_score_history":
             return [self.ep_score_history[i] for i in idx]
-        if name in ("num_arms", "max_num_objects", "seed"):
+        if name in RUNTIME_PARAMS:
+            if name in envs.PROGRESS_REQUIRED + ("base_reward",) and not self.progress:
+                raise AttributeError(f"{self.env_class} has no attribute {name!r}")
+            v = self.get_param(name)
+            return [v for _ in idx]
+        if name in ARENA_SCALARS:
+            st, A, K = self._arena_field(name)
+            rec = self.get_state()
+            out = []
+            for i in idx:
+                v = float(st.fields(A, K, st.unpack(A, K, rec[i])[0])[name][0])
+                out.append(np.array([v]) if name == "conveyor_speed" else v)  # base_env.py:186 keeps an array
+            return out
+        if name == "seed":
+            return [int(self.seeds_used[i]) for i in idx]
+        if name in ("num_arms", "max_num_objects", "control_frequency"):
             return [self.env_kwargs[name] for _ in idx]
+        if name == "frame_skip":
+            return [int((1 / self.env_kwargs["control_frequency"]) / 0.001) for _ in idx]
+        if name == "dt":
+            return [0.001 * int((1 / self.env_kwargs["control_frequency"]) / 0.001) for _ in idx]
+        if name in ("observation_space", "action_space"):
+            return [getattr(self, name) for _ in idx]
+        if all(name in self._user_attrs[i] for i in idx):
+            return [self._user_attrs[i][name] for i in idx]
         raise AttributeError(name)
 
     def set_attr(self, name, value, indices=None):
-        raise AttributeError(f"{name} is fixed at creation on the GPU path")
+        """SB3 VecEnv.set_attr.  Runtime scalars of the env (pt_time, conveyor parameters, force threshold, spawn
+        parameters, reward factors) are one value per handle: they may be set for all envs at once (or for a subset
+        when the value does not change).  play_time / conveyor_speed are per-arena state.  num_arms,
+        max_num_objects, seed and control_frequency fixed the compiled scene and raise.  Any other name is stored
+        as a plain attribute of the envs (as setattr on the reference env would), with no effect on the step."""
+        idx = self._indices(indices)
+        if name in RUNTIME_PARAMS:
+            v = float(np.asarray(value).reshape(-1)[0])
+            if len(set(idx)) != self.num_envs and v != self.get_param(name):
+                raise ValueError(f"{name} is one value for all {self.num_envs} arenas of the batch: set it on every env")
+            _lib.check(self._L.fm_set_param(self._h, name.encode(), v))
+            return
+        if name in ARENA_SCALARS:
+            st, A, K = self._arena_field(name)
+            rec = self.get_state()
+            vals = np.broadcast_to(np.asarray(value, dtype=np.float64).reshape(-1), (len(idx),)) \
+                if np.ndim(value) <= 1 and np.size(value) in (1, len(idx)) else None
+            if vals is None:
+                raise ValueError(f"{name}: one value, or one per index")
+            for j, i in enumerate(idx):
+                d, ints, rng = st.unpack(A, K, rec[i])
+                st.fields(A, K, d)[name][0] = vals[j]
+                rec[i] = st.pack(A, K, d, ints, rng)
+            self.set_state(rec)
+            return
+        if name in FIXED_ATTRS:
+            raise ValueError(f"{name} is fixed when the arenas are created (compiled scene / frame_skip / seeds)")
+        for i in idx:
+            self._user_attrs[i][name] = value
 
-    def env_method(self, method_name, *args, indices=None, **kwargs):
-        if method_name == "reset":
-            n = self.num_envs
-            mask = np.zeros(n, np.uint8)
-            mask[list(range(n)) if indices is None else indices] = 1
-            self.reset(mask=mask)
-            return [None] * int(mask.sum())
-        raise AttributeError(method_name)
+    # per-arena methods of the reference env with a batch-path equivalent (env_method)
+    def _m_reset(self, idx, *args, **kwargs):
+        n = self.num_envs
+        mask = np.zeros(n, np.uint8)
+        mask[idx] = 1
+        obs = self.reset(mask=mask)
+        obs = obs if isinstance(obs, np.ndarray) else obs.cpu().numpy()
+        return [(obs[i].copy(), {}) for i in idx]  # gymnasium reset(): (obs, info)
+
+    def _m_render(self, idx, *args, **kwargs):
+        return self.get_images(idx, **kwargs)
+
+    def _m_get_wrapper_attr(self, idx, name):
+        return self.get_attr(name, idx)
+
+    def _m_set_wrapper_attr(self, idx, name, value):
+        self.set_attr(name, value, idx)
+        return [None] * len(idx)
+
+    def _m_seed(self, idx, seed=None):
+        return [None if seed is None else int(seed) for _ in idx]
+
+    def _m_close(self, idx):
+        return [None] * len(idx)
+
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        """SB3 VecEnv.env_method: call `method_name` on every env in `indices`, one result per env.  The per-arena
+        methods of the reference env that exist on the batch path: reset (masked fm_reset; (obs, {}) per env),
+        render (rgb_array), get_wrapper_attr / set_wrapper_attr (get_attr / set_attr), seed, close.  Methods that
+        would step or rebuild one arena on its own (step, reset_sim's physics internals) have no per-arena form:
+        the batch steps every arena in one launch."""
+        idx = self._indices(indices)
+        m = getattr(self, "_m_" + method_name, None)
+        if m is None:
+            raise AttributeError(f"env_method({method_name!r}): no per-arena form on the GPU path "
+                                 "(available: reset, render, get_wrapper_attr, set_wrapper_attr, seed, close)")
+        out = m(idx, *method_args, **method_kwargs)
+        return out if isinstance(out, list) else [out] * len(idx)
 
     # ------------------------------------------------------------------ rendering (rendering.py, base_env.py:288)
     def render_tensors(self, indices=None, width=480, height=480, camera=None, frames=False):
@@ -380,3 +513,27 @@ class FactoryVecEnv:
             self.close()
         except Exception:
             pass
+
+
+def make_vec_env(env_id, n_envs=1, seed=None, start_index=0, monitor_dir=None, wrapper_class=None, env_kwargs=None,
+                 vec_env_cls=None, vec_env_kwargs=None, monitor_kwargs=None, wrapper_kwargs=None):
+    """stable_baselines3.common.env_util.make_vec_env (SB3 2.3.2 signature), building thunks of
+    factory_marl_amd.environments specs: env_id is an env class (or a callable returning a spec, as learning.py's
+    lambda) or a class name; vec_env_cls defaults to FactoryVecEnv.  monitor_dir / wrapper_class are not provided:
+    the batch env reports the Monitor episodes itself."""
+    if monitor_dir is not None or wrapper_class is not None:
+        raise NotImplementedError("make_vec_env: monitor_dir / wrapper_class are not provided on the batch path")
+    env_kwargs = dict(env_kwargs or {})
+    if isinstance(env_id, str):
+        env_id = getattr(envs, env_id)
+
+    def make_env(rank):
+        def _init():
+            return env_id(**env_kwargs)
+        return _init
+
+    fns = [make_env(i + start_index) for i in range(n_envs)]
+    vec = (vec_env_cls or FactoryVecEnv)(fns, **(vec_env_kwargs or {}))
+    if seed is not None:
+        vec.seed(seed)
+    return vec

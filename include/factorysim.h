@@ -108,6 +108,16 @@ const char* fm_last_error(void);
 int fm_set_stream(fm_handle* h, void* stream);
 int fm_sync(fm_handle* h);
 
+/* Runtime-mutable scalars (SB3 VecEnv.set_attr / get_attr on the reference env's attributes, base_env.py:133-141,
+ * environments.py:276-282): "pt_time", "initial_conveyor_speed", "conveyor_acceleration",
+ * "force_contact_threshold", "spawn_freq_increase", "init_spawn_freq" (= spawn_freq * num_arms),
+ * "gripper_to_closest_cube_reward_factor", "closest_cube_to_bucket_reward_factor",
+ * "small_action_norm_reward_factor", "base_reward".  Global to the handle; launches queued after the call use the
+ * new value.  control_frequency (frame_skip), num_arms, max_num_objects and seeds are fixed at fm_create.
+ * Per-arena dynamic values (play_time, conveyor_speed, spawn_freq) live in the state record (fm_set_state). */
+int fm_set_param(fm_handle* h, const char* name, double value);
+int fm_get_param(const fm_handle* h, const char* name, double* value);
+
 int fm_obs_dim(const fm_handle* h);
 int fm_act_dim(const fm_handle* h);
 int fm_num_arenas(const fm_handle* h);

@@ -278,7 +278,7 @@ int or_ik_plan_flat(int A, int n_in, const int* in_scene, const double* cube_qpo
                     double* ad, double* tpos, double* tquat, int* close) {
   or_ik_arm p;
   arm_from_flat(&p, ai, ad);
-  or_ik_in in = {A, n_in, in_scene, cube_qpos, cube_qvel, grip, base, bucket, arm_q};
+  or_ik_in in = {A, n_in, in_scene, cube_qpos, cube_qvel, grip, base, bucket, arm_q, 0.2, 0.001 * 100};
   int r = or_ik_plan(&in, &p, tpos, tquat, close);
   arm_to_flat(&p, ai, ad);
   return r;
@@ -290,6 +290,13 @@ void or_ik_finish_flat(int* ai, double* ad, int success, const double* q7, int c
   arm_to_flat(&p, ai, ad);
 }
 int or_env_act_dim(const or_env* e) { return e->act_dim; }
+/* BaseEnv(pt_time=..., control_frequency=...) (base_env.py:28-31,133-135): the low-pass time constant, frame_skip
+ * = int((1 / control_frequency) / timestep), and everything that follows env.dt (play time, conveyor speed, the IK
+ * policy's step counts and compensation) */
+void or_env_set_timing(or_env* e, double pt_time, double control_frequency) {
+  e->t.pt_time = pt_time;
+  e->t.frame_skip = (int)((1.0 / control_frequency) / 0.001);
+}
 int or_env_ik_steps(const or_env* e) { return e->ik_steps; }
 void or_env_ik_arm(const or_env* e, int i, int* ai, double* ad) { arm_to_flat(&e->ik[i], ai, ad); }
 
@@ -317,7 +324,7 @@ int or_ik_compose_replay(const or_model* m, int* arm_i /* A x 19 */, double* arm
   or_ik_arm ik[OR_IK_MAXA];
   for (int i = 0; i < m->A; i++) arm_from_flat(&ik[i], arm_i + 19 * i, arm_d + 11 * i);
   rec_solver r = {rec_success, rec_q7, n_rec, 0, args_out};
-  or_ik_compose(m, ik, qpos, qvel, grip, base, in_scene, n_in, rec_solve, &r, arm_ctrl);
+  or_ik_compose(m, ik, qpos, qvel, grip, base, in_scene, n_in, rec_solve, &r, 0.2, 0.001 * 100, arm_ctrl);
   for (int i = 0; i < m->A; i++) arm_to_flat(&ik[i], arm_i + 19 * i, arm_d + 11 * i);
   return r.calls;
 }

@@ -46,12 +46,13 @@ const double OR_IK_DEFAULT_POSE[8] = {-0.5, -0.5, 0.0, 1.0, 0.0, -1.6, 0.0, 0.06
 #define TARGET_THRESHOLD 0.05
 #define RELEASE_THRESHOLD 0.1
 #define GRASP_OFFSET 0.04
-#define RELEASE_WAIT 5  /* int(0.5 / 0.1) */
-#define GRASP_WAIT 10   /* int(1.0 / 0.1) */
-#define MOVE_STEPS 10   /* int(1.0 / 0.1) */
-#define TIMEOUT_STEPS 30 /* int(3.0 / 0.1) */
-
-static double pt_compensation(void) { return 0.2 * 0.1 * 15.0; } /* env.pt_time * env.dt * 15.0 */
+/* the step counts and the velocity compensation follow env.dt and env.pt_time (ik_policy.py:56-67); at the
+ * defaults (dt = 0.001 * 100 = 0.1, pt_time 0.2): release 5, grasp 10, move 10, timeout 30, 0.30000000000000004 */
+#define RELEASE_WAIT ((int)(0.5 / in->dt))
+#define GRASP_WAIT ((int)(1.0 / in->dt))
+#define MOVE_STEPS ((int)(1.0 / in->dt))
+#define TIMEOUT_STEPS ((int)(3.0 / in->dt))
+#define PT_COMPENSATION (in->pt_time * in->dt * 15.0) /* env.pt_time * env.dt * 15.0 */
 
 static double norm3d(const double* a) { return sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
 
@@ -259,8 +260,8 @@ int or_ik_plan(const or_ik_in* in, or_ik_arm* p, double tpos[3], double tquat[4]
     return 0;
   }
   if (comp) {
-    tp[0] += ov[0] * pt_compensation();
-    tp[1] += ov[1] * pt_compensation();
+    tp[0] += ov[0] * PT_COMPENSATION;
+    tp[1] += ov[1] * PT_COMPENSATION;
   }
   memcpy(tpos, tp, sizeof tp);
   memcpy(tquat, target_quat, sizeof target_quat);

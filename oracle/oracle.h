@@ -185,6 +185,7 @@ typedef struct or_ik_in {
   const double* base;       /* site_xpos of player_site */
   const double* bucket;     /* xpos of this arm's bucket (buckets[i % 2]) */
   const double* arm_q;      /* the 7 hinge qpos */
+  double pt_time, dt;       /* env.pt_time, env.dt = timestep * frame_skip (ik_policy.py:56-67) */
 } or_ik_in;
 extern const double OR_IK_DEFAULT_POSE[8];
 void or_ik_arm_init(or_ik_arm* p);
@@ -197,7 +198,7 @@ int or_ik_solve(const or_model* m, or_data* scratch, const double* qpos, int arm
 typedef int (*or_ik_solver)(void* ctx, int arm, const double* tpos, const double* tquat, double* q7);
 void or_ik_compose(const or_model* m, or_ik_arm* ik, const double* qpos, const double* qvel, const double* grip /*3A*/,
                    const double* base /*3A*/, const int* in_scene, int n_in, or_ik_solver solve, void* ctx,
-                   double* arm_ctrl /* 8A */);
+                   double pt_time, double dt, double* arm_ctrl /* 8A */);
 void or_compose_class(const or_model* m, int env_class, const float* action, const double* ik, const int* ik_state,
                       const double* ik_actions, double* pause_last, double* arm_ctrl);
 
@@ -220,6 +221,7 @@ typedef struct or_env {
   double ep_return;
   int ep_len;
 } or_env;
+void or_env_set_timing(or_env* e, double pt_time, double control_frequency);
 
 or_env* or_env_create(int A, int K, uint64_t seed, int env_class, const double* reward_w /*4*/);
 void or_env_free(or_env* e);

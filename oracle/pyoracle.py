@@ -46,7 +46,7 @@ def _bind(L, real):
         DP = C.POINTER(real)
         sig = {
             "or_env_create": (P, [I, I, U64, I, DP]),
-            "or_env_free": (None, [P]),
+            "or_env_free": (None, [P]), "or_env_set_timing": (None, [P, D, D]),
             "or_env_reset": (None, [P, P]),
             "or_env_step": (I, [P, P, P, DP, DP]),
             "or_env_model": (P, [P]), "or_env_data": (P, [P]), "or_env_task": (P, [P]),
@@ -310,7 +310,7 @@ class Env:
     """Oracle restatement of the env classes of src/environments.py (default AllFullRLProgressRewardEnv)."""
 
     def __init__(self, num_arms=2, max_num_objects=4, seed=42, reward="progress",
-                 weights=(0.2, 0.4, 0.0, 0.4), env_class=None, f32=False):
+                 weights=(0.2, 0.4, 0.0, 0.4), env_class=None, f32=False, pt_time=0.2, control_frequency=10):
         L = self.L = lib(f32)
         w = (L.c_real * 4)(*weights)
         if env_class is None:  # legacy selector: progress -> AllFullRL, score -> FactoryManipulationEnv
@@ -319,6 +319,8 @@ class Env:
         self.h = L.or_env_create(num_arms, max_num_objects, seed, ENV_CLASSES[env_class], w)
         if not self.h:
             raise ValueError("bad env config")
+        if (pt_time, control_frequency) != (0.2, 10):
+            L.or_env_set_timing(self.h, pt_time, control_frequency)
         self.model = Model(num_arms, max_num_objects, seed, handle=L.or_env_model(self.h), L=L)
         self.data = Data(self.model, handle=L.or_env_data(self.h))
         self.task = L.or_env_task(self.h)

@@ -344,7 +344,7 @@ or_env* or_env_create(int A, int K, uint64_t seed, int env_class, const double* 
  * is a callback: qpos_from_site_pose in the env (or_ik_solve), recorded results in the golden replay. */
 void or_ik_compose(const or_model* m, or_ik_arm* ik, const double* qpos, const double* qvel, const double* grip,
                    const double* base, const int* in_scene, int n_in, or_ik_solver solve, void* ctx,
-                   double* arm_ctrl /* 8A */) {
+                   double pt_time, double dt, double* arm_ctrl /* 8A */) {
   const int A = m->A, K = m->K;
   double cq[64 * 7], cv[64 * 6];
   for (int k = 0; k < K; k++) {
@@ -354,7 +354,8 @@ void or_ik_compose(const or_model* m, or_ik_arm* ik, const double* qpos, const d
   for (int i = 0; i < A; i++) {
     or_ik_arm* p = &ik[i];
     const double bucket[3] = {(i % 2) == 0 ? 0.9 : -0.9, 0.7 - (A / 2 - 1), 1.05 - 0.04};
-    or_ik_in in = {A, n_in, in_scene, cq, cv, grip + 3 * i, base + 3 * i, bucket, qpos + 1 + 7 * K + 9 * i};
+    or_ik_in in = {A, n_in, in_scene, cq, cv, grip + 3 * i, base + 3 * i, bucket, qpos + 1 + 7 * K + 9 * i,
+                   pt_time, dt};
     double tp[3], tq[4], ctrl[8];
     int close = 0;
     if (or_ik_plan(&in, p, tp, tq, &close)) {
@@ -389,7 +390,8 @@ static void ik_compose(or_env* e, double* arm_ctrl) {
     memcpy(base + 3 * i, e->d->site_xpos + 3 * m->base_site[i], 3 * sizeof(double));
   }
   e->ik_steps = 0;
-  or_ik_compose(m, e->ik, e->d->qpos, e->d->qvel, grip, base, e->t.in_scene, e->t.n_in, env_ik_solve, e, arm_ctrl);
+  or_ik_compose(m, e->ik, e->d->qpos, e->d->qvel, grip, base, e->t.in_scene, e->t.n_in, env_ik_solve, e, e->t.pt_time,
+                0.001 * e->t.frame_skip, arm_ctrl);
   for (int i = 0; i < m->A; i++)
     for (int o = 0; o < m->A; o++) e->t.ik_ignore[i][o] = e->ik[i].ignore[o];
 }

@@ -43,7 +43,13 @@ def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights
 def gpu_env(n, precision, A, K, env_class="AllFullRLProgressRewardEnv", **kw):
     from factory_marl_amd import FactoryVecEnv
 
-    ekw = dict(num_arms=A, max_num_objects=K, seed=42, small_action_norm_reward_factor=0.1)
+    from factory_marl_amd.environments import run_kwargs
+
+    # the oracle rollouts' reward weights (rollout(): grip 0.2, bucket 0.4, action 0.1, base 0.4)
+    ekw = run_kwargs(env_class, num_arms=A, max_num_objects=K, seed=42)
+    if "small_action_norm_reward_factor" in ekw:
+        ekw["small_action_norm_reward_factor"] = 0.1
+    ekw.update(kw.pop("env_kwargs", {}))
     env = FactoryVecEnv(n, env_class=env_class, env_kwargs=ekw, precision=precision, **kw)
     env.reset()
     return env
@@ -111,4 +117,6 @@ def summary(r, gate=1e-4):
                 worst=float(e.max()), int_bad=len(r["int_bad"]), flag_bad=len(r["flag_bad"]),
                 obs_worst=float(r["obs_err"].max()), rew_worst=float(r["rew_err"].max()) if len(r["rew_err"]) else 0.0,
                 contacts_dropped=int(r["counters"][:, 0].sum()), terminations=r["terms"], max_cubes=r["max_cubes"],
+                newton_iters_per_substep=round(float(r["counters"][:, 1].sum()) / (100.0 * len(r["counters"])), 3),
+                newton_maxit_hits=int(r["counters"][:, 2].sum()),
                 missing_steps=[int(s) for s in r["err_steps"][e > gate]])

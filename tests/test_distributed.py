@@ -90,3 +90,37 @@ def test_bench_diagnostics_arithmetic():
     assert d["mean_contacts_per_substep"] == 1.0 and d["max_contacts_in_a_substep"] == 9
     assert d["mean_objects_in_scene"] == 2.5 and d["episodes_ended"] == 2
     assert bench.algorithmic_bytes(2, 4) == 120480
+
+
+def _run_bench(*args):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run", *args], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("scaling,ranges,total", [("weak", [[0, 4096], [4096, 8192]], 8192),
+                                                  ("strong", [[0, 2048], [2048, 4096]], 4096)])
+def test_bench_gpus_flag_launches_ranks(scaling, ranges, total):
+    """`bench.py --gpus 2` (no torchrun environment) starts two rank processes itself: the line reports
+    n_gpus 2, the ranks own disjoint arena ids (weak: 4096 each; strong: the 4096 total split), and the job
+    clock is the slower rank's"""
+    d = _run_bench("--gpus", "2", "--scaling", scaling, "--steps", "10")
+    assert d["n_gpus"] == 2 and d["backend"] == "gloo"
+    assert d["rank_arenas"] == ranges and d["total_arenas"] == total
+    assert d["wall_max"] == 1.5 and d["value"] == pytest.approx(total * 10 / 1.5)
+
+
+def test_bench_single_rank_and_config4_split():
+    d = _run_bench("--steps", "4")
+    assert d["n_gpus"] == 1 and d["rank_arenas"] == [[0, 4096]]
+    d4 = _run_bench("--gpus", "2", "--workload", "config4")
+    assert d4["scaling"] == "strong" and d4["rank_arenas"] == [[0, 65536], [65536, 131072]]

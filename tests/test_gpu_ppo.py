@@ -18,9 +18,10 @@ def _have_gpu():
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 def test_ppo_iterations_on_gpu_env():
     from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.environments import run_kwargs
     from factory_marl_amd.ppo import PPO
 
-    env = FactoryVecEnv(512, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42))
+    env = FactoryVecEnv(512, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=2, max_num_objects=4, seed=42))
     ppo = PPO(env, n_steps=8, batch_size=1024, n_epochs=2, seed=0)
     ppo.learn(512 * 8 * 2)
     assert ppo.num_timesteps == 512 * 8 * 2 and len(ppo.logs) == 2
@@ -43,7 +44,8 @@ def test_reference_policy_drives_gpu_env(run):
     pol = ActorCriticPolicy.for_env(env, net_arch=meta["net_arch"]).to(env.device)
     sd = {k: torch.as_tensor(v) for k, v in np.load(os.path.join(GOLD, f"policy_{run}.npz")).items()}
     pol.load_state_dict(sd)
-    obs = env.reset().clone()
+    env.reset()
+    obs = env.obs.clone()
     ret = torch.zeros(256, device=env.device)
     ended = 0
     scores = []

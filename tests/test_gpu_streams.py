@@ -14,8 +14,9 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(),
 
 def _env(n=64):
     from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.environments import run_kwargs
 
-    env = FactoryVecEnv(n, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42), precision="fp32")
+    env = FactoryVecEnv(n, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=2, max_num_objects=4, seed=42), precision="fp32")
     env.reset()
     return env
 

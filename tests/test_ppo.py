@@ -159,3 +159,34 @@ def test_data_parallel_ppo_gloo_world2():
     np.testing.assert_array_equal(out[0][2], out[1][2])
     assert out[0][3] == out[1][3] == 32 * 8 * 2 * 3
     assert out[0][4] == out[1][4] == 2 * 32  # episodes of 8 steps: every arena of both ranks ended once
+
+
+def _identical_arenas_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    env = ToyEnv(n=16, seed=0)  # the SAME arenas on both ranks (bench / FactoryVecEnv default: seed 42 everywhere)
+    ppo = PPO(env, policy_kwargs=dict(net_arch=(16, 16)), n_steps=4, batch_size=32, n_epochs=1, seed=3, dist=dist)
+    buf, _ = ppo.collect_rollouts()
+    q.put((rank, buf["actions"].numpy()))
+    dist.destroy_process_group()
+
+
+def test_ranks_sample_different_actions_on_identical_arenas():
+    """data-parallel ranks with identical arenas and broadcast weights still draw independent actions (a per-rank
+    sampling stream): their rollouts differ, so the global batch holds world x independent samples"""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_identical_arenas_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted((q.get(timeout=300) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+    a0, a1 = out[0][1], out[1][1]
+    assert a0.shape == a1.shape
+    assert not np.array_equal(a0, a1)

@@ -29,7 +29,8 @@ def main():
         if term:
             e.reset()
     recs, acts = np.stack(recs), np.stack(acts)
-    kw = dict(num_arms=A, max_num_objects=K, seed=42, small_action_norm_reward_factor=0.1)
+    kw = dict(num_arms=A, max_num_objects=K, seed=42, gripper_to_closest_cube_reward_factor=0.2,
+              closest_cube_to_bucket_reward_factor=0.4, small_action_norm_reward_factor=0.1, base_reward=0.4)
     outs = {}
     for mode in ["dyn", "fixed"]:
         os.environ["FM_FORCE_DYNAMIC"] = "1" if mode == "dyn" else "0"

@@ -15,11 +15,13 @@ po.build()
 rng = np.random.default_rng(7)
 e = po.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4))
 ref0 = e.reset()
-env = FactoryVecEnv(1, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42, small_action_norm_reward_factor=0.1),
+env = FactoryVecEnv(1, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42, gripper_to_closest_cube_reward_factor=0.2,
+                                     closest_cube_to_bucket_reward_factor=0.4, small_action_norm_reward_factor=0.1,
+                                     base_reward=0.4),
                     precision=prec)
 obs = env.reset()
 torch.cuda.synchronize()
-print("reset obs max diff", np.abs(obs.cpu().numpy()[0] - ref0).max(), flush=True)
+print("reset obs max diff", np.abs(np.asarray(obs)[0] - ref0).max(), flush=True)
 nq, nv, nu, nd, ni = st.sizes(A, K)
 g0 = st.unpack(A, K, env.get_state()[0])
 d0, i0, r0 = e.export_state()

@@ -7,6 +7,7 @@ import torch
 sys.path.insert(0, ".")
 from oracle import pyoracle as po  # noqa: E402  (test infrastructure: checker only)
 from factory_marl_amd import FactoryVecEnv, state as st  # noqa: E402
+from factory_marl_amd.environments import run_kwargs  # noqa: E402
 
 A, K = 2, 4
 prec = sys.argv[1] if len(sys.argv) > 1 else "fp64"
@@ -18,7 +19,7 @@ e.reset()
 rng = np.random.default_rng(3)
 for t in range(nsteps):
     e.step(rng.uniform(-2, 2, 8 * A).astype(np.float32))
-env = FactoryVecEnv(1, env_kwargs=dict(num_arms=A, max_num_objects=K, seed=42), precision=prec)
+env = FactoryVecEnv(1, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=A, max_num_objects=K, seed=42), precision=prec)
 env.reset()
 d, i, r = e.export_state()
 env.set_state(st.pack(A, K, d, i, r)[None])

@@ -4,7 +4,8 @@ solver setting, one JSON line per trajectory (tests/parity_util.summary + the se
 
 usage: FACTORYSIM_LIB=path python tools/parity_sweep.py --prec fp32 [--tol 1e-9] [--tag name]
            [--traj A,K,T,seed ...]        (default: 2,4,96,7  2,4,300,21  2,8,300,5  2,10,250,9)
-Trajectories are cached as .npz under gpurun_out/traj/ so several processes share one oracle rollout.
+Trajectories are cached as .npz under gpurun_out/traj/ (or $FM_TRAJ_CACHE: a cache made in the container travels
+with the tree) so several processes share one oracle rollout.
 """
 import argparse
 import json
@@ -22,7 +23,7 @@ import parity_util as pu  # noqa: E402
 from oracle import pyoracle as po  # noqa: E402  (checker)
 
 
-def load_traj(A, K, T, seed, cache=os.path.join(ROOT, "gpurun_out", "traj")):
+def load_traj(A, K, T, seed, cache=os.environ.get("FM_TRAJ_CACHE", os.path.join(ROOT, "gpurun_out", "traj"))):
     os.makedirs(cache, exist_ok=True)
     f = os.path.join(cache, f"traj_{A}_{K}_{T}_{seed}.npz")
     if os.path.exists(f):
@@ -59,7 +60,7 @@ def main():
         r = pu.compare(traj, args.prec, A, K, solver_tolerance=args.tol, solver_iterations=args.iters)
         s = pu.summary(r)
         s.update(tag=args.tag, lib=os.path.basename(os.environ.get("FACTORYSIM_LIB", "libfactorysim.so")),
-                 prec=args.prec, tol=args.tol, noise_guard=os.environ.get("FM_NO_NOISE_GUARD") != "1",
+                 prec=args.prec, tol=args.tol,
                  traj=spec, rollout_s=round(t1 - t0, 1), gpu_s=round(time.time() - t1, 1))
         print(json.dumps(s), flush=True)
 

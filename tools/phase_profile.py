@@ -24,8 +24,10 @@ def main():
     import torch
 
     from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.environments import run_kwargs
 
-    env = FactoryVecEnv(args.arenas, env_kwargs=dict(num_arms=args.arms, max_num_objects=args.objects, seed=42),
+    env = FactoryVecEnv(args.arenas, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=args.arms,
+                                                           max_num_objects=args.objects, seed=42),
                         precision=args.precision)
     env.reset()
     import bench

@@ -18,8 +18,9 @@ a = ap.parse_args()
 import torch  # noqa: E402
 
 from factory_marl_amd import FactoryVecEnv  # noqa: E402
+from factory_marl_amd.environments import run_kwargs  # noqa: E402
 
-env = FactoryVecEnv(a.arenas, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42),
+env = FactoryVecEnv(a.arenas, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=2, max_num_objects=4, seed=42),
                     seeds=np.arange(a.arenas))
 env.reset()
 g = torch.Generator(device="cuda").manual_seed(0)

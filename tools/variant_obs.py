@@ -8,8 +8,9 @@ import torch
 
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from factory_marl_amd import FactoryVecEnv  # noqa: E402
+from factory_marl_amd.environments import run_kwargs  # noqa: E402
 
-env = FactoryVecEnv(4096, env_kwargs=dict(num_arms=2, max_num_objects=4, seed=42), precision="fp32")
+env = FactoryVecEnv(4096, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=2, max_num_objects=4, seed=42), precision="fp32")
 env.reset()
 g = torch.Generator(device=env.device)
 g.manual_seed(0)
