@@ -84,6 +84,8 @@ struct fm_handle {
   bool prof_on = false;
   int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
   Lay lay_step{};  // workspace layout of the env-step kernel in use
+  bool spill = false;          // DimsSpill: Hessian + contact records in per-arena global scratch (fp64, > 160 KiB)
+  char* spill_buf = nullptr;   // [N][lay.gtotal]
 };
 
 template <typename T>
@@ -106,8 +108,8 @@ static int upload_raw(fm_handle* h, U** dst, const std::vector<U>& src) {
   return 0;
 }
 
-static Lay lds_layout(const Dims& d, int tsize) {
-  return make_layout(d.A, d.K, d.nq, d.nv, d.nu, d.ngc, d.ncb, d.maxcon, d.maxrow, d.ntree, tsize);
+static Lay lds_layout(const Dims& d, int tsize, bool spill = false) {
+  return make_layout(d.A, d.K, d.nq, d.nv, d.nu, d.ngc, d.ncb, d.maxcon, d.maxrow, d.ntree, tsize, spill);
 }
 
 template <typename T>
@@ -182,6 +184,8 @@ static State<T> make_state(const fm_handle* h) {
   S.counters = h->counters;
   S.cost = h->cost;
   S.order = h->order;
+  S.spill = h->spill_buf;
+  S.spill_stride = h->spill ? h->lay.gtotal : 0;
   return S;
 }
 
@@ -329,7 +333,26 @@ static int create_typed(fm_handle* h) {
     h->allocs.push_back(h->order);
   }
   h->lay = lds_layout(d, sizeof(T));
-  if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
+  if (h->lay.total > 160 * 1024) {
+    if constexpr (sizeof(T) == 8) {
+      // fp64 scenes beyond the CU's LDS (4 arms): the parity-grade spill layout (DimsSpill, fm_dev.hpp)
+      h->lay = lds_layout(d, sizeof(T), true);
+      if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
+      h->spill = true;
+      HIPCHK(hipMalloc((void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay.gtotal));
+      h->allocs.push_back(h->spill_buf);
+      HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, DimsSpill>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 h->lay.total));
+      HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, DimsSpill, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
+      HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, DimsSpill, false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
+      h->lay_step = h->lay;
+      return 0;
+    } else {
+      return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
+    }
+  }
   HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              h->lay.total));
   // env-step kernel: a compile-time specialisation when the scene is one of FM_FIXED_SCENES
@@ -467,6 +490,15 @@ static void launch_step(fm_handle* h, const StepIO& io) {
   FM_FIXED_SCENES
 #undef X
   (void)idx;
+  if constexpr (sizeof(T) == 8) {
+    if (h->spill) {
+      if (ik)
+        hipLaunchKernelGGL((step_kernel<T, DimsSpill, true>), grid, block, h->lay.total, h->stream, pd);
+      else
+        hipLaunchKernelGGL((step_kernel<T, DimsSpill, false>), grid, block, h->lay.total, h->stream, pd);
+      return;
+    }
+  }
   if (ik)
     hipLaunchKernelGGL((step_kernel<T, Dims, true>), grid, block, h->lay.total, h->stream, pd);
   else
@@ -722,7 +754,10 @@ int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
   dim3 grid(h->dm.N), block(WAVE);
-  if (h->fp64) {
+  if (h->fp64 && h->spill) {
+    hipLaunchKernelGGL((reset_kernel<double, DimsSpill>), grid, block, h->lay.total, h->stream, make_model<double>(h),
+                       make_state<double>(h), h->lay, obs, mask);
+  } else if (h->fp64) {
     hipLaunchKernelGGL((reset_kernel<double, Dims>), grid, block, h->lay.total, h->stream, make_model<double>(h),
                        make_state<double>(h), h->lay, obs, mask);
   } else {
@@ -791,7 +826,12 @@ int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int c
   double* dbuf = nullptr;
   HIPCHK(hipMalloc(&dbuf, need * sizeof(double)));
   HIPCHK(hipMemset(dbuf, 0, need * sizeof(double)));
-  if (h->fp64) {
+  if (h->fp64 && h->spill) {
+    HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double, DimsSpill>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
+    hipLaunchKernelGGL((debug_kernel<double, DimsSpill>), dim3(1), dim3(WAVE), h->lay.total, h->stream,
+                       make_model<double>(h), make_state<double>(h), h->lay, arena, actuated, dbuf);
+  } else if (h->fp64) {
     HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                h->lay.total));
     hipLaunchKernelGGL((debug_kernel<double, Dims>), dim3(1), dim3(WAVE), h->lay.total, h->stream, make_model<double>(h),

@@ -59,6 +59,7 @@ constexpr int MAXPC = 8;      // contacts per geom pair (box-box)
 // Flat per-arena record layouts (strides in elements)
 struct Dims {
   static constexpr bool fixed = false;  // runtime dims (see FixedDims for compile-time scenes)
+  static constexpr bool spill = false;  // Hessian + contact records in LDS (see DimsSpill)
   static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
@@ -129,7 +130,19 @@ struct State {
   // order[b]; cost[a] = arena a's last env-step in s_memrealtime ticks.  Null: workgroup b steps arena b.
   gptr<uint32_t> cost{nullptr};
   cptr<int32_t> order{nullptr};
+  // DimsSpill: per-arena global scratch blocks (Lay::gtotal bytes each) for the Hessian and the contact records
+  gptr<char> spill{nullptr};
+  long long spill_stride{0};
 };
+
+// the arena's global scratch block (nullptr unless the kernel runs a DimsSpill layout)
+template <typename DIM, typename T>
+__device__ __forceinline__ char* spill_base(const State<T>& S, int arena) {
+  if constexpr (DIM::spill)
+    return (char*)S.spill + (long long)arena * S.spill_stride;
+  else
+    return nullptr;
+}
 
 struct StepIO {
   cptr<float> actions;
@@ -205,6 +218,8 @@ struct Lay {
   int prof;   // uint64 [16]  phase clocks of this arena (profiling only)
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int total;
+  // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
+  int spill, gtotal;
 };
 
 // fp32 builds place the world origin of the float copies at z = 1 m (the table / belt height): contact
@@ -424,7 +439,7 @@ struct StepParams {
 // lane-address register instead of one address register per array.
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
-                                              int maxrow, int ntree, int tsize) {
+                                              int maxrow, int ntree, int tsize, bool spill = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -468,7 +483,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   // float64 vectors (gradient, M (a - as), scratch; live from the solve to the integration) are never live
   // together
   const int u0 = off;
-  L.H = take(tsize * nv * nv);
+  if (!spill) L.H = take(tsize * nv * nv);
   L.g = take(8 * nv);
   L.Ma = take(8 * nv);
   L.tmp = take(8 * nv);
@@ -484,7 +499,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   uend = off > uend ? off : uend;
   off = uend;
   L.c_i = take(4 * 4 * maxcon);
-  L.c_r = take(tsize * CR_N * maxcon);
+  if (!spill) L.c_r = take(tsize * CR_N * maxcon);
   L.r_i = take(4 * 4 * maxrow);
   L.r_r = take(tsize * RR_N * maxrow);
   L.tmask = take(8 * ntree * ((maxcon + 63) / 64));  // word h of tree t at [h * ntree + t]
@@ -494,14 +509,31 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.scal = take(8 * 4);
   L.prof = take(8 * 16);
   L.total = off;
+  if (spill) {  // the two largest arrays in the arena's global scratch block (L2 / HBM) instead of LDS
+    L.spill = 1;
+    L.H = 0;
+    L.c_r = (tsize * nv * nv + 15) & ~15;
+    L.gtotal = L.c_r + ((tsize * CR_N * maxcon + 255) & ~255);
+  }
   return L;
 }
 
 // compile-time scene dimensions for the configurations the library specialises (A arms, K objects);
 // runtime-only quantities stay members
+// runtime dims whose arena workspace exceeds the CU's LDS (fp64 at 4 arms: the dense Newton Hessian alone is
+// 141.5 KB at (4, 16)): the Hessian and the contact records live in a per-arena global scratch block (L2-resident,
+// flat/global accesses; the wave's program order covers their hand-offs at SYNC() as it does for LDS), everything
+// else in LDS.  The parity-grade fp64 build of those scenes.
+struct DimsSpill : Dims {
+  static constexpr bool spill = true;
+  DimsSpill() = default;
+  __host__ __device__ DimsSpill(const Dims& d) : Dims(d) {}
+};
+
 template <int A_, int K_>
 struct FixedDims {
   static constexpr bool fixed = true;
+  static constexpr bool spill = false;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;

@@ -71,6 +71,7 @@ template <typename T, typename DIM>
 struct Ws {
   char* base;
   const Lay* L;
+  char* gbase = nullptr;  // DimsSpill: this arena's global scratch block (H, contact records)
   __device__ __forceinline__ T* q() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -379,6 +380,8 @@ struct Ws {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
       return (T*)(base + c.H);
+    } else if constexpr (DIM::spill) {
+      return (T*)(gbase + L->H);
     } else {
       return (T*)(base + L->H);
     }
@@ -395,6 +398,8 @@ struct Ws {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
       return (T*)(base + c.c_r);
+    } else if constexpr (DIM::spill) {
+      return (T*)(gbase + L->c_r);
     } else {
       return (T*)(base + L->c_r);
     }
@@ -1793,7 +1798,9 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     R = R > T(1e-15) ? R : T(1e-15);
     cr[CR_MU] = mu;
     cr[CR_D] = T(1) / R;
-    cr[CR_KD] = Kk * imp * dist;
+    // pyramid edges: the position term of aref with K / (4 mu^2), pinned by MuJoCo's resting equilibria and
+    // belt-carried velocities in the reference runs (oracle/solver.c, tests/test_physics_pins.py)
+    cr[CR_KD] = Kk * imp * dist / (T(4) * mu * mu);
     cr[CR_BD] = Bb;
   }
   SYNC();
@@ -3580,7 +3587,7 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   const int arena = blockIdx.x;
   const DIM dm(M.dm);
   if (mask && !mask[arena]) return;
-  Ws<T, DIM> w{lds_base(smem), &L};
+  Ws<T, DIM> w{lds_base(smem), &L, spill_base<DIM>(S, arena)};
   int32_t* ti = S.ints + (size_t)arena * dm.int_stride;
   double* td = S.dbl + (size_t)arena * dm.dbl_stride + dm.nu;
   int64_t* ctr = S.counters + FM_NCTR * (size_t)arena;
@@ -3625,7 +3632,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   const int A = dm.A, K = dm.K, nu = dm.nu;
   // a fresh opaque LDS base per use: workspace addresses are recomputed inside each phase instead of
   // being hoisted out of the substep loop (which would keep every phase's addresses live everywhere)
-#define w (Ws<T, DIM>{lds_base(smem), &L})
+#define w (Ws<T, DIM>{lds_base(smem), &L, spill_base<DIM>(S, arena)})
   if (M.prof && LANE < 16) w.prof()[LANE] = LANE == PH_LAST ? wall_clock64() : 0ull;
   if (LANE == 0) {
     w.misc()[MISC_CSUM] = 0;
@@ -3756,13 +3763,14 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
     SYNC();
     for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, false>(M, w, e / 10, e % 10);
     SYNC();
-    // stage state for the next env-step = state before the TaskManager's teleports
-    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.qd()[i];
-    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.vd()[i];
     if (LANE == 0) task_tail(M, w, ti, td, rng, ctr, act);
     FULL_SYNC();
     SYNC();
     refresh_copies(M, w);  // the TaskManager's teleports wrote the master state
+    // stage state for the next env-step = the state after the TaskManager's teleports: MuJoCo's own outputs in
+    // the reference show a cube spawned from rest falling freely from its first substep (tests/test_physics_pins.py)
+    for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.qd()[i];
+    for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.vd()[i];
     SYNC();
     if (IK && env_toggle(ec)) ik_proposals(M, w, ti, td);  // the step's observation (environments.py:197, 560-577)
     const int term = sc_[1] != 0.0;
@@ -3856,7 +3864,7 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
                                                    double* out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const DIM dm(M.dm);
-  Ws<T, DIM> w{lds_base(smem), &L};
+  Ws<T, DIM> w{lds_base(smem), &L, spill_base<DIM>(S, arena)};
   int64_t* ctr = S.counters + FM_NCTR * (size_t)arena;
   const double* ph = S.phys + (size_t)arena * dm.phys_stride;
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;

@@ -6,6 +6,13 @@
  *   solref -> K = 1/(dmax^2 tc^2 dr^2), B = 2/(dmax tc) with tc >= 2 dt (refsafe);
  *   solimp -> impedance d(|pos - margin|) (getimpedance);  R = max(MINVAL, (1-d)/d * diagApprox);
  *   diagApprox from body/dof invweight0 (mj_diagApprox; pyramid edges: tran*(1 + mu^2));
+ *   pyramid edges: the position term of aref uses K / (4 mu^2) -- PINNED by MuJoCo's own outputs in the reference
+ *   (runs/[run].zip _last_obs, tests/test_physics_pins.py): cubes resting on the belt (mu 0.8, solref 0.004,
+ *   solimp 0.95) sit 2.29e-6 m deep and on the table (mu 1, solref 0.002, solimp 0.98) 4.19e-7 m deep, where
+ *   K imp pos alone gives 2.56x / 4.1x shallower equilibria, while the belt-carried cube velocities (set by the
+ *   edges' R, B and J) already match MuJoCo to 1 float32 ulp.  The 1 / (4 mu^2) position stiffness reproduces all
+ *   three to float32 resolution; scaling R by 4 mu^2 instead fits the depths but moves the carried velocities by
+ *   3-4 ulps.  MuJoCo's source is not available to state the general form (OR_PYR_KSCALE);
  *   aref = -B*efc_vel - K*d*(pos - margin).
  * Solver: minimises the MuJoCo primal cost
  *   f(a) = 1/2 (a - a0)^T M (a - a0) + sum_i 1/2 D_i (J_i a - aref_i)^2 [eq, or ineq with J_i a < aref_i]
@@ -23,6 +30,9 @@
 #define OR_SOLVER_TOL 1e-12 /* liboracle_f32.so (fp32 floor study) overrides it */
 #endif
 #define OR_SOLVER_ITER 100
+#ifndef OR_PYR_KSCALE
+#define OR_PYR_KSCALE(mu) (4.0 * (mu) * (mu)) /* pyramid edges: aref position stiffness K / this (header comment) */
+#endif
 
 double or_impedance(const double si[5], double x) {
   double dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
@@ -59,7 +69,7 @@ static void kbip(const or_model* m, const double solref[2], const double solimp[
 }
 
 static int add_row(const or_model* m, or_data* d, int type, int id, double pos, double margin, double diag,
-                   const double solref[2], const double solimp[5]) {
+                   const double solref[2], const double solimp[5], double kscale) {
   int r = d->nefc++;
   d->efc_type[r] = type;
   d->efc_id[r] = id;
@@ -70,7 +80,7 @@ static int add_row(const or_model* m, or_data* d, int type, int id, double pos, 
   double K, B;
   kbip(m, solref, solimp, &K, &B);
   d->efc_imp[r] = imp;
-  d->efc_K[r] = K;
+  d->efc_K[r] = K / kscale;
   d->efc_B[r] = B;
   double R = (1 - imp) * diag / imp;
   d->efc_R[r] = R > OR_MINVAL ? R : OR_MINVAL;
@@ -89,7 +99,7 @@ void or_make_constraint(const or_model* m, or_data* d) {
     double pos = (d->qpos[m->jnt_qposadr[j0]] - m->qpos0[m->jnt_qposadr[j0]]) -
                  (d->qpos[m->jnt_qposadr[j1]] - m->qpos0[m->jnt_qposadr[j1]]);
     double diag = m->dof_invweight0[d0] + m->dof_invweight0[d1];
-    int r = add_row(m, d, OR_CNSTR_EQUALITY, e, pos, 0.0, diag, m->eq_solref + 2 * e, m->eq_solimp + 5 * e);
+    int r = add_row(m, d, OR_CNSTR_EQUALITY, e, pos, 0.0, diag, m->eq_solref + 2 * e, m->eq_solimp + 5 * e, 1.0);
     double* J = d->efc_J + (size_t)r * nv;
     memset(J, 0, nv * sizeof(double));
     J[d0] = 1.0;
@@ -104,7 +114,7 @@ void or_make_constraint(const or_model* m, or_data* d) {
       double dist = side == 0 ? q - m->jnt_range[2 * j] : m->jnt_range[2 * j + 1] - q;
       if (dist < 0.0) {
         int r = add_row(m, d, OR_CNSTR_LIMIT, j, dist, 0.0, m->dof_invweight0[da], m->jnt_solref + 2 * j,
-                        m->jnt_solimp + 5 * j);
+                        m->jnt_solimp + 5 * j, 1.0);
         double* J = d->efc_J + (size_t)r * nv;
         memset(J, 0, nv * sizeof(double));
         J[da] = side == 0 ? 1.0 : -1.0;
@@ -130,7 +140,8 @@ void or_make_constraint(const or_model* m, or_data* d) {
         Jf[k][i] = f[0] * (jp2[i] - jp1[i]) + f[1] * (jp2[nv + i] - jp1[nv + i]) + f[2] * (jp2[2 * nv + i] - jp1[2 * nv + i]);
     }
     for (int e = 0; e < 4; e++) {
-      int r = add_row(m, d, OR_CNSTR_PYRAMIDAL, c, con->dist, con->margin, diag, con->solref, con->solimp);
+      int r = add_row(m, d, OR_CNSTR_PYRAMIDAL, c, con->dist, con->margin, diag, con->solref, con->solimp,
+                      OR_PYR_KSCALE(mu));
       double* J = d->efc_J + (size_t)r * nv;
       int t = 1 + e / 2;
       double sg = (e & 1) ? -mu : mu;

@@ -533,10 +533,15 @@ int or_env_step(or_env* e, const float* action, float* obs, double* reward, doub
     }
     or_step1(m, d);
   }
-  memcpy(e->stage_qpos, d->qpos, m->nq * sizeof(double));
-  memcpy(e->stage_qvel, d->qvel, m->nv * sizeof(double));
   or_task_step(t, m, d->qpos, d->qvel);
   or_task_after_step(t);
+  /* the TaskManager's teleports (spawn / hide) are seen by the next substep's dynamics: MuJoCo's own outputs in
+   * the reference show a cube spawned from rest on the floor falling freely from its first substep (its
+   * (z, vz) after n env-steps is exact free fall over 100 n substeps, tests/test_physics_pins.py), not held for one
+   * substep by the pre-teleport floor contact -- so the stage is recomputed at the post-teleport state */
+  or_step1(m, d);
+  memcpy(e->stage_qpos, d->qpos, m->nq * sizeof(double));
+  memcpy(e->stage_qvel, d->qvel, m->nv * sizeof(double));
   int terminated = t->failure_counter > 0 || force_term;
   double grip[48];
   for (int i = 0; i < m->A; i++) memcpy(grip + 3 * i, d->site_xpos + 3 * m->grip_site[i], 3 * sizeof(double));

@@ -1,7 +1,7 @@
 """Policy fixtures from the reference's own checkpoints (runs/*.zip, stable-baselines3 2.3.2 saves).
 
 Only policy.pth (a torch state_dict) is read, with torch.load(weights_only=True) -- nothing in the
-archive is executed.  Two runs are kept as float32 .npz data: rk5rxnav (AllFullRLProgressRewardEnv,
+archive is executed.  All four runs are kept as float32 .npz data, e.g. rk5rxnav (AllFullRLProgressRewardEnv,
 2 arms x 10 cubes, Box(16) actions, obs 178) and y6lp1j7k (PauseIKToggleEnv, 4 arms x 10 cubes,
 MultiDiscrete([2]*4), obs 258).  Usage: python tests/golden/gen_policy_fixtures.py
 """
@@ -18,7 +18,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 
 if __name__ == "__main__":
     meta = {}
-    for run in ["rk5rxnav", "y6lp1j7k"]:
+    for run in ["rk5rxnav", "r666unuv", "xfwgqibb", "y6lp1j7k"]:
         with zipfile.ZipFile(os.path.join(REF, f"{run}.zip")) as z:
             sd = torch.load(io.BytesIO(z.read("policy.pth")), weights_only=True, map_location="cpu")
         cfg = json.load(open(os.path.join(REF, f"{run}.json")))

@@ -297,20 +297,24 @@ def test_impedance_curve(oracle):
 def test_ik_base_policy_scores_end_to_end(oracle):
     """system-level known answer: FactoryManipulationEnv (every arm on the IK base policy, ik_policy.py) over
     the oracle's own physics, kinematics and DLS IK picks cubes off the belt and drops them into the buckets
-    -- the behaviour the reference's base policy exists for.  Measured: 5 cubes scored (3 + 2) in 300
-    env-steps from reset, both arms scoring, every FSM state visited."""
+    -- the behaviour the reference's base policy exists for.  Measured (physics pinned by the reference runs,
+    tests/test_physics_pins.py): both buckets score in the first episode ((1, 1) by env-step 157, where a contact
+    force above 200 N on an arm ends it), every FSM state visited; report.tex:276-282 averages (1.65, 1.17) over
+    208.8 env-steps for this policy on the reference's MuJoCo"""
     import numpy as np
 
     e = oracle.Env(2, 4, 42, env_class="FactoryManipulationEnv")
     e.reset()
     seen = set()
     total = 0.0
-    for _ in range(300):
+    for t in range(300):
         _, r, term, _, info = e.step(np.zeros(0, np.float32))
         total += r
         seen |= {e.ik_arm(i)["state"] for i in range(2)}
-        assert not term
-    assert info["scores"][0] >= 2 and info["scores"][1] >= 1 and total == sum(info["scores"])
+        if term:
+            break
+    assert t >= 100
+    assert info["scores"][0] >= 1 and info["scores"][1] >= 1 and total == sum(info["scores"])
     assert seen == set(range(7))
 
 
@@ -318,7 +322,7 @@ def test_float_restatement_floor(oracle):
     """the oracle's algorithm in plain single precision (liboracle_f32.so: every double a float), teacher-forced
     from the float64 oracle's (2, 4) trajectory: the fp32 floor the GPU fp32 build is judged against
     (tests/test_gpu_parity.py).  It misses the SURVEY gate at the landing impacts of freshly spawned cubes
-    (env-steps 4-5 and 52-53 after reset) and keeps integer task state exact"""
+    (env-steps 4-8 and 52-57 after reset) and keeps integer task state exact"""
     import os
     import sys
 
@@ -327,5 +331,5 @@ def test_float_restatement_floor(oracle):
 
     s = fp32_floor.summarize(fp32_floor.float_oracle_study(2, 4, 96, 7))
     assert s["flips"] == 0
-    assert {4, 5, 52, 53} <= set(s["missing_steps"])
-    assert 0.85 <= s["within"] <= 0.95  # measured 90.6 %, median 6.7e-5
+    assert {4, 52} <= set(s["missing_steps"])
+    assert 0.85 <= s["within"] <= 0.95  # measured 90.6 %, median 6.3e-5
