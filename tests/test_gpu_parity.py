@@ -288,3 +288,37 @@ def test_config5_scene_4x16_pause_toggle_fp32(oracle):
     # spacing (4.8e-7 m) in the contact points of their resting contacts shows up as spin noise of those
     # (task-irrelevant) cubes; the fp64 build is the parity build for this scene shape
     assert frac >= 0.65
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("env_class", ["PauseIKToggleEnv", "BackupIKToggleEnv"])
+def test_teacher_forced_ik_classes_fp64_4x16(oracle, env_class):
+    """BASELINE config 5's scene (4 arms x 16 cubes, environments.py:580-645, ik_policy.py:141-282) in the
+    parity-grade fp64 build: the arena exceeds the CU's 160 KiB of LDS in float64, so the Newton Hessian and the
+    contact records run from a per-arena global scratch block (DimsSpill, fm_dev.hpp).  150 teacher-forced
+    env-steps: IK FSM block and every integer exact, IK doubles within 1e-6, state within 1e-5"""
+    traj = pu.rollout(oracle, 4, 16, 150, seed_actions=13, env_class=env_class)
+    r = pu.compare(traj, "fp64", 4, 16, env_class, verbose_tol=1e-6)
+    print(f"fp64 (4,16) {env_class}: worst rel err {r['errs'].max():.3e}, obs {r['obs_err'].max():.2e}, "
+          f"IK block {r['ik_err'].max():.2e}, terms {r['terms']}, max contacts {int(r['counters'][:, 5].max())}")
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    assert r["errs"].max() <= 1e-5
+    assert r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
+    assert r["ik_err"].max() <= 1e-6
+    assert r["counters"][:, 0].sum() == 0
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_ik_timing_follows_control_frequency_and_pt_time(oracle):
+    """ik_policy.py:56-67 derives the IK policy's step counts (release 0.5 s, grasp 1 s, move 1 s, timeout 3 s) and its
+    velocity compensation (pt_time * dt * 15) from env.dt and env.pt_time: at control_frequency 20 Hz (frame_skip 50:
+    10 / 20 / 20 / 60 env-steps) and pt_time 0.3 the GPU IK FSM stays exact with the oracle's"""
+    kw = dict(pt_time=0.3, control_frequency=20)
+    traj = pu.rollout(oracle, 2, 4, 300, seed_actions=13, env_class="PauseIKToggleEnv", env_kw=kw)
+    r = pu.compare(traj, "fp64", 2, 4, "PauseIKToggleEnv", verbose_tol=1e-6, env_kwargs=kw)
+    ints = np.stack([o["ints"] for o in traj[2]])
+    states = set(ints[:, 2 * 4 + 11::5].ravel().tolist())
+    print(f"20 Hz / pt_time 0.3: worst {r['errs'].max():.2e}, IK block {r['ik_err'].max():.2e}, states {sorted(states)}")
+    assert {0, 1, 2, 3} <= states
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    assert r["errs"].max() <= 1e-5 and r["ik_err"].max() <= 1e-6

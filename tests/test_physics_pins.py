@@ -69,6 +69,10 @@ def _cube(s, k):
 
 
 def test_free_fall_after_spawn_matches_mujoco(ref, still_run):
+    check_free_fall(ref, still_run)
+
+
+def check_free_fall(ref, still_run):
     """every reference cube in free fall on the spawn column (x, y) = (0, 1) equals the oracle's fall after a spawn:
     the first spawn of an episode (teleported during reset's forward, task_utils.py:137) and a later one"""
     traj = []
@@ -87,6 +91,10 @@ def test_free_fall_after_spawn_matches_mujoco(ref, still_run):
 
 
 def test_resting_depth_on_the_belt_matches_mujoco(ref, still_run):
+    check_belt_depth(ref, still_run)
+
+
+def check_belt_depth(ref, still_run):
     """cubes riding the belt: MuJoCo's box-box soft-contact equilibrium (belt geom: priority 1, solref 0.004,
     solimp 0.95..0.9999, friction 0.8) for every cube size seen in the runs, to float32 resolution"""
     sizes = ref["sizes"]
@@ -113,38 +121,48 @@ def test_resting_depth_on_the_belt_matches_mujoco(ref, still_run):
     assert all(abs(d - 2.2814e-6) < 2e-9 for d in depth.values()), depth
 
 
-def test_resting_depth_on_the_table_matches_mujoco(oracle, ref):
-    """a cube resting on the table top (table geom: priority 1, solref 0.002, solimp 0.98..0.9999, friction 1):
-    two reference workers hold one each (xfwgqibb worker 4, y6lp1j7k worker 4)"""
+def table_rows(ref):
     sizes = ref["sizes"]
     table = [(p, v) for _, _, p, v in ref["rows"] if abs(p[2] - 1.0 - sizes[np.argmin(np.abs(p[2] - 1.0 - sizes))]) < 1e-5
              and np.abs(v).max() < 1e-6]
     assert len(table) == 2
-    from factory_marl_amd import state as st  # noqa: F401  (record layout only)
+    return [(1.0 + sizes[int(np.argmin(np.abs(p[2] - 1.0 - sizes)))] - p[2]) for p, _ in table]
 
+
+TABLE_CUBE = 9  # last in the spawn queue: never spawned within the test
+
+
+def table_start(d, sizes):
+    """the state record's float64 block with cube TABLE_CUBE placed 1 um deep on the table top, at rest"""
+    nq = 1 + 7 * K + 9 * A
+    k = TABLE_CUBE
+    dd = d.copy()
+    dd[1 + 7 * k:8 + 7 * k] = [-0.41, -0.275, 1.0 + sizes[k] - 1e-6, 1, 0, 0, 0]
+    dd[nq + 1 + 6 * k:nq + 7 + 6 * k] = 0
+    return dd
+
+
+def test_resting_depth_on_the_table_matches_mujoco(oracle, ref):
+    """a cube resting on the table top (table geom: priority 1, solref 0.002, solimp 0.98..0.9999, friction 1):
+    two reference workers hold one each (xfwgqibb worker 4, y6lp1j7k worker 4); the depth does not depend on the
+    cube's size (as on the belt), so the scene's cube TABLE_CUBE stands in for both"""
+    sizes = ref["sizes"]
     e = oracle.Env(A, K, 42, weights=(0.2, 0.4, 0.0, 0.4))
     e.reset()
     d, i, r = e.export_state()
-    k = 9  # last in the spawn queue: never spawned in this test
-    nq = 1 + 7 * K + 9 * A
-    for p, _ in table:
-        j = int(np.argmin(np.abs(p[2] - 1.0 - sizes)))
-        dd = d.copy()
-        # the same size as the reference cube: the scene's cube k has size sizes[k]; place it so that its resting
-        # height is compared through the depth (independent of size, as on the belt)
-        dd[1 + 7 * k:8 + 7 * k] = [-0.41, -0.275, 1.0 + sizes[k] - 1e-6, 1, 0, 0, 0]
-        dd[nq + 1 + 6 * k:nq + 7 + 6 * k] = 0
-        e.import_state(dd, i, r)
-        for _ in range(30):
-            e.step(np.zeros(8 * A, np.float32))
-        z = e.export_state()[0][1 + 7 * k + 2]
-        depth = 1.0 + sizes[k] - z
-        ref_depth = 1.0 + sizes[j] - p[2]
+    e.import_state(table_start(d, sizes), i, r)
+    for _ in range(30):
+        e.step(np.zeros(8 * A, np.float32))
+    depth = 1.0 + sizes[TABLE_CUBE] - e.export_state()[0][1 + 7 * TABLE_CUBE + 2]
+    for ref_depth in table_rows(ref):
         assert abs(depth - ref_depth) <= 1.0 * ULP_Z, (depth, ref_depth)
-        e.reset()
 
 
 def test_belt_carried_velocity_matches_mujoco(ref, still_run):
+    check_carried_velocity(ref, still_run)
+
+
+def check_carried_velocity(ref, still_run):
     """the belt-riding cubes' velocity (speed ramp 0.1 + 1e-4 n, implicit velocity actuator, load, tangential
     coupling): the reference workers' values equal the oracle's at some episode step n to ~1 float32 ulp (the load
     on the belt differs between the reference workers and this run by a few cubes: ~1 ulp per 0.1 kg)"""
