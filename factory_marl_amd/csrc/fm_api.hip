@@ -80,6 +80,8 @@ struct fm_handle {
   float* cube_rgba = nullptr;    // [N][K][4]
   float* render_frames = nullptr;
   int* render_arenas = nullptr;
+  int* render_arenas_host = nullptr;   // pinned staging of the arena list (async H2D on the stream)
+  hipEvent_t render_copied = nullptr;  // the last staging copy has been consumed
   size_t render_cap = 0;          // arenas the scratch holds
   bool prof_on = false;
   int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
@@ -117,6 +119,7 @@ static Model<T> make_model(const fm_handle* h) {
   Model<T> M;
   M.dm = h->dm;
   M.dt = T(0.001);
+  M.timestep = 0.001;
   M.grav = T(9.81);
   M.belt_mass = T(1000);
   M.belt_kv = T(1e4);
@@ -164,13 +167,13 @@ static Model<T> make_model(const fm_handle* h) {
   M.cbp = h->cbp;
   for (int a = 0; a < 5; a++)
     for (int b = 0; b < 5; b++) M.ptab[5 * a + b] = h->sc.ptab[a][b];
-  M.param = (const T*)h->param;
+  M.param = (const double*)h->param;
   M.cube = (const T*)h->cube;
   M.meaninertia = (const T*)h->meaninertia;
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
   const char* cl = getenv("FM_CHOL_LDS");
-  M.dbg_flags = (cl && cl[0] == '1') ? 1 : 0;
+  M.dbg_flags = (cl && cl[0] == '1') ? 1 : ((cl && cl[0] == '2') ? 2 : 0);
   return M;
 }
 
@@ -291,7 +294,7 @@ static int create_typed(fm_handle* h) {
     if ((r = upload_raw<uint16_t>(h, &h->cbg, s.cb_geoms))) return r;
     if ((r = upload_raw<uint32_t>(h, &h->cbp, s.cb_pairs))) return r;
   }
-  if ((r = upload<T>(h, &h->param, param))) return r;
+  if ((r = upload<double>(h, &h->param, param))) return r;
   if ((r = upload<T>(h, &h->cube, s.cube))) return r;
   if ((r = upload<T>(h, &h->meaninertia, s.meaninertia))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->tri, s.tri))) return r;
@@ -674,6 +677,8 @@ void fm_destroy(fm_handle* h) {
   for (void* p : h->allocs) (void)hipFree(p);
   for (void* p : {(void*)h->render_rgb, (void*)h->cube_rgba, (void*)h->render_frames, (void*)h->render_arenas})
     if (p) (void)hipFree(p);
+  if (h->render_arenas_host) (void)hipHostFree(h->render_arenas_host);
+  if (h->render_copied) (void)hipEventDestroy(h->render_copied);
   if (h->handoff) (void)hipEventDestroy(h->handoff);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);  // never a stream the caller handed in
   delete h;
@@ -903,19 +908,30 @@ int fm_render(fm_handle* h, const int32_t* arenas, int count, int width, int hei
     HIPCHK(hipMemcpy(h->cube_rgba, h->sc.cube_rgba.data(), h->sc.cube_rgba.size() * sizeof(float),
                      hipMemcpyHostToDevice));
   }
+  if (!h->render_copied) HIPCHK(hipEventCreateWithFlags(&h->render_copied, hipEventDisableTiming));
   if ((size_t)count > h->render_cap) {
+    // growing the scratch frees buffers queued work may still read: the one synchronising path (rare)
     HIPCHK(hipStreamSynchronize(h->stream));
     if (h->render_frames) HIPCHK(hipFree(h->render_frames));
     if (h->render_arenas) HIPCHK(hipFree(h->render_arenas));
+    if (h->render_arenas_host) HIPCHK(hipHostFree(h->render_arenas_host));
     h->render_frames = nullptr;
     h->render_arenas = nullptr;
+    h->render_arenas_host = nullptr;
     HIPCHK(hipMalloc((void**)&h->render_frames, (size_t)count * h->dm.ngc * RF_N * sizeof(float)));
     HIPCHK(hipMalloc((void**)&h->render_arenas, (size_t)count * sizeof(int)));
+    HIPCHK(hipHostMalloc((void**)&h->render_arenas_host, (size_t)count * sizeof(int), hipHostMallocDefault));
     h->render_cap = count;
+  } else {
+    // the staging buffer is reused: wait only for the previous render's arena copy (not for the stream)
+    HIPCHK(hipEventSynchronize(h->render_copied));
   }
-  // the arena list is read by the kernel on the stream: a synchronous copy, ordered after queued work
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(h->render_arenas, arenas, (size_t)count * sizeof(int), hipMemcpyHostToDevice));
+  // the arena list travels through pinned staging on the stream, ordered after queued env-steps; the caller's
+  // array is free again when this call returns
+  std::memcpy(h->render_arenas_host, arenas, (size_t)count * sizeof(int));
+  HIPCHK(hipMemcpyAsync(h->render_arenas, h->render_arenas_host, (size_t)count * sizeof(int), hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipEventRecord(h->render_copied, h->stream));
   // MuJoCo free camera (mjv_cameraInModel): forward from azimuth / elevation, eye = lookat - distance * forward;
   // default = the reference viewer's initial camera (scene.py:164-169), fovy 45 deg
   const float def[6] = {-0.30914206f, -0.14805237f, 1.53675732f, 3.6720494f, 66.957422f, -28.843359f};

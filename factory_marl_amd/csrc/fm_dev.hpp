@@ -87,6 +87,7 @@ struct Model {
   // scene scalars
   T dt, grav;
   T belt_mass, belt_kv, belt_damp, belt_invw_t;
+  double timestep;  // model.opt.timestep, exact (solver gains)
   double init_speed, accel, pt_time, force_thr, spawn_freq0, spawn_inc;
   double w_grip, w_bucket, w_action, base_reward;
   double bucket_x0, bucket_x1, bucket_y, bucket_z;
@@ -110,13 +111,14 @@ struct Model {
   cptr<uint16_t> cbg;   // geoms grouped by collision body
   cptr<uint32_t> cbp;   // [ncbp] allowed collision-body pairs b1 | b2 << 8
   int ptab[25];          // param index by (pclass g1, pclass g2)
-  cptr<T> param;     // [nparam][8] mu, solref(2), solimp(5)
+  cptr<double> param;  // [nparam][8] mu, solref(2), solimp(5): float64 in both builds (impedance / R below)
   // per arena
   cptr<T> cube;      // [N][K][4] h, m, I, pad
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
-  int dbg_flags;             // diagnostics: bit 0 = LDS Cholesky instead of the register one (FM_CHOL_LDS=1)
+  int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one
+                             // instead of the dense matrix-core one for runtime-dims fp32 (FM_CHOL_LDS=2)
 };
 
 template <typename T>

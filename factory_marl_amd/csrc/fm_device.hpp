@@ -1780,28 +1780,30 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     ci[2] = tb;
     ci[3] = pidx | (armflag << 16) | (nda << 20) | (ndb << 24);
     // parameters
-    const T* prm = M.param + 8 * pidx;
-    T mu = prm[0];
-    T dist = cr[CR_DIST];
-    T imp = impedance(prm + 3, dist);
-    T Kk, Bb;
-    kb_params(M.dt, prm + 1, prm + 3, Kk, Bb);
-    auto invw_t = [&](int kb) -> T {
-      if (kb == 0) return T(0);
-      if (kb == 1) return M.belt_invw_t;
-      if (kb < 2 + K) return T(1) / w.cube()[4 * (kb - 2) + 1];
-      return M.body[32 * ((kb - 2 - K) % 10) + 28];
+    // impedance, R and the reference acceleration's gains in float64 in both builds: near solimp's dmax = 0.9999
+    // the factor (1 - imp) of R keeps 4 significant digits in float (and 0.9999 itself rounds by 1.7e-4 of it)
+    const double* prm = M.param + 8 * pidx;
+    const double mu = prm[0];
+    const double dist = (double)cr[CR_DIST];
+    const double imp = impedance(prm + 3, dist);
+    double Kk, Bb;
+    kb_params(M.timestep, prm + 1, prm + 3, Kk, Bb);
+    auto invw_t = [&](int kb) -> double {
+      if (kb == 0) return 0.0;
+      if (kb == 1) return (double)M.belt_invw_t;
+      if (kb < 2 + K) return 1.0 / (double)w.cube()[4 * (kb - 2) + 1];
+      return (double)M.body[32 * ((kb - 2 - K) % 10) + 28];
     };
-    T tran = invw_t(kb1) + invw_t(kb2);
-    T diag = tran + mu * mu * tran;
-    T R = (T(1) - imp) * diag / imp;
-    R = R > T(1e-15) ? R : T(1e-15);
-    cr[CR_MU] = mu;
-    cr[CR_D] = T(1) / R;
+    const double tran = invw_t(kb1) + invw_t(kb2);
+    const double diag = tran + mu * mu * tran;
+    double R = (1.0 - imp) * diag / imp;
+    R = R > 1e-15 ? R : 1e-15;
+    cr[CR_MU] = (T)mu;
+    cr[CR_D] = (T)(1.0 / R);
     // pyramid edges: the position term of aref with K / (4 mu^2), pinned by MuJoCo's resting equilibria and
     // belt-carried velocities in the reference runs (oracle/solver.c, tests/test_physics_pins.py)
-    cr[CR_KD] = Kk * imp * dist / (T(4) * mu * mu);
-    cr[CR_BD] = Bb;
+    cr[CR_KD] = (T)(Kk * imp * dist / (4.0 * mu * mu));
+    cr[CR_BD] = (T)Bb;
   }
   SYNC();
   // efc velocity in the contact frame
@@ -1842,8 +1844,8 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
       const uint64_t bal = __ballot(act);
       const int slot = nr + __popcll(bal & below);
       if (act && slot < dm.maxrow) {
-        const T sr[2] = {eq ? T(0.002) : T(0.02), T(1.0)};
-        const T si[5] = {eq ? T(0.98) : T(0.9), eq ? T(0.9999) : T(0.95), T(0.001), T(0.5), T(2.0)};
+        const double sr[2] = {eq ? 0.002 : 0.02, 1.0};
+        const double si[5] = {eq ? 0.98 : 0.9, eq ? 0.9999 : 0.95, 0.001, 0.5, 2.0};
         int* ri = w.ri() + 4 * slot;
         T* rr = w.rr() + RR_N * slot;
         ri[0] = d0;
@@ -1852,14 +1854,14 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
         rr[RR_C0] = c0;
         rr[RR_C1] = c1;
         rr[RR_POS] = pos;
-        const T imp = impedance(si, pos);
-        T Kk, Bb;
-        kb_params(M.dt, sr, si, Kk, Bb);
-        T R = (T(1) - imp) * diag / imp;
-        R = R > T(1e-15) ? R : T(1e-15);
-        rr[RR_D] = T(1) / R;
-        const T vel = c0 * v[d0] + (d1 >= 0 ? c1 * v[d1] : T(0));
-        rr[RR_AREF] = -Bb * vel - Kk * imp * pos;
+        const double imp = impedance(si, (double)pos);
+        double Kk, Bb;
+        kb_params(M.timestep, sr, si, Kk, Bb);
+        double R = (1.0 - imp) * (double)diag / imp;
+        R = R > 1e-15 ? R : 1e-15;
+        rr[RR_D] = (T)(1.0 / R);
+        const double vel = (double)c0 * (double)v[d0] + (d1 >= 0 ? (double)c1 * (double)v[d1] : 0.0);
+        rr[RR_AREF] = (T)(-Bb * vel - Kk * imp * (double)pos);
       }
       nr += __popcll(bal);
     }
@@ -2417,6 +2419,174 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
   return true;
 }
 
+// fp32 runtime-dims scenes with nv > 64 ((4,16): 133 dofs): dense right-looking Cholesky over 16-wide column
+// blocks of H (LDS, row-major, original numbering; only the lower triangle is read or written), the trailing
+// update on the matrix cores.  Per block b (columns c0 .. c0 + 15):
+//  * the 16 x 16 diagonal block is factored in registers on lanes 0..15 (lane j owns row j; pivots broadcast by
+//    v_readlane), written back with the pivots' reciprocals;
+//  * the panel below it, L[r][blk] = H[r][blk] L_bb^-T, one row per lane (the L_bb entries are uniform LDS reads);
+//  * the trailing lower triangle H -= L_panel L_panel' tile by tile, one 16 x 16 tile = 4 chained
+//    v_mfma_f32_16x16x4_f32 whose A and B operands are panel entries (A[i][k] = L[16I + i][c0 + k],
+//    B[k][j] = L[16J + j][c0 + k]).
+// The sparse LDS path spends 3 wave barriers and a ballot compaction per pivot (133 pivots); this one spends 3
+// per block (9 blocks) and ~120 tile products.  The substitutions run blockwise the same way.
+template <typename T, typename DIM>
+__device__ constexpr bool dense_mfma_chol() {
+  return sizeof(T) == 4 && !DIM::fixed;
+}
+template <typename DIM>
+__device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* H, const int nv, const double* g,
+                                                float* dir) {
+  const int j = LANE;
+  const int nb = (nv + 15) >> 4;
+  float* dinv = (float*)w.tmp();  // quad()'s scratch, dead until the line search
+  const float tiny = 1e-37f;
+  for (int b = 0; b < nb; b++) {
+    const int c0 = 16 * b;
+    const int bw = nv - c0 < 16 ? nv - c0 : 16;
+    // ---- diagonal block: lane j < bw holds row c0 + j (lower entries at (max, min))
+    float col[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int hi = i > j ? i : j, lo = i > j ? j : i;
+      col[i] = (j < bw && i < bw) ? H[(c0 + hi) * nv + c0 + lo] : 0.0f;
+    }
+    float di = 1.0f;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (k < bw) {
+        float d = readlane(col[k], k);
+        d = d > tiny ? d : tiny;
+        const float ri = 1.0f / sqrtf(d);
+        const float lj = col[k] * ri;  // lane j > k: L[j][k]; lane k: L[k][k]
+        if (j == k) di = ri;
+        if (j >= k) col[k] = lj;
+        if (j > k) {
+          float lv[16];
+#pragma unroll
+          for (int i = 0; i < 16; i++) lv[i] = i > k ? readlane(lj, i) : 0.0f;
+#pragma unroll
+          for (int i = 0; i < 16; i++)
+            if (i > k) col[i] -= lv[i] * lj;
+        }
+      }
+    }
+    SYNC();  // every lane has read its block before it is overwritten
+    if (j < bw) {
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k <= j) H[(c0 + j) * nv + c0 + k] = col[k];
+      dinv[c0 + j] = di;
+    }
+    SYNC();
+    // ---- panel: rows below the block, one per lane
+    for (int r = c0 + bw + j; r < nv; r += WAVE) {
+      float x[16];
+      float* Hr = H + r * nv + c0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) x[k] = k < bw ? Hr[k] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        if (k < bw) {
+          float s = x[k];
+          const float* Lk = H + (c0 + k) * nv + c0;
+#pragma unroll
+          for (int m = 0; m < k; m++) s -= x[m] * Lk[m];
+          x[k] = s * dinv[c0 + k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < bw) Hr[k] = x[k];
+    }
+    SYNC();
+    // ---- trailing update, lower-triangle tiles (I >= J) of the rows after the block
+    const int t0 = b + 1;
+    const int nt = nb - t0;
+    const int ntile = nt * (nt + 1) / 2;
+    const int li = j & 15, lk = j >> 4;
+    for (int t = 0; t < ntile; t++) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) I++;
+      const int J = t - I * (I + 1) / 2;
+      const int rI = 16 * (t0 + I), rJ = 16 * (t0 + J);
+      fm_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; s++) {
+        const int c = c0 + 4 * s + lk;
+        const bool cok = c < c0 + bw;
+        const float a = (cok && rI + li < nv) ? H[(rI + li) * nv + c] : 0.0f;
+        const float bb = (cok && rJ + li < nv) ? H[(rJ + li) * nv + c] : 0.0f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+      }
+      const int cc = rJ + li;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int rr = rI + 4 * lk + q;
+        if (rr < nv && cc < nv && rr >= cc) H[rr * nv + cc] -= acc[q];
+      }
+    }
+    SYNC();
+  }
+  // ---- forward substitution L y = -g (y in dir), block by block
+  for (int r = j; r < nv; r += WAVE) dir[r] = (float)-g[r];
+  SYNC();
+  for (int b = 0; b < nb; b++) {
+    const int c0 = 16 * b;
+    const int bw = nv - c0 < 16 ? nv - c0 : 16;
+    float acc = j < bw ? dir[c0 + j] : 0.0f;
+    const float dj = j < bw ? dinv[c0 + j] : 1.0f;
+    float y = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (k < bw) {
+        const float yk = readlane(acc * dj, k);
+        if (j == k) y = yk;
+        if (j > k && j < bw) acc -= H[(c0 + j) * nv + c0 + k] * yk;
+      }
+    }
+    SYNC();
+    if (j < bw) dir[c0 + j] = y;
+    SYNC();
+    for (int r = c0 + bw + j; r < nv; r += WAVE) {
+      const float* Lr = H + r * nv + c0;
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < bw) s += Lr[k] * dir[c0 + k];
+      dir[r] -= s;
+    }
+    SYNC();
+  }
+  // ---- backward substitution L' x = y, last block first
+  for (int b = nb - 1; b >= 0; b--) {
+    const int c0 = 16 * b;
+    const int bw = nv - c0 < 16 ? nv - c0 : 16;
+    float acc = j < bw ? dir[c0 + j] : 0.0f;
+    const float dj = j < bw ? dinv[c0 + j] : 1.0f;
+    float x = 0.0f;
+#pragma unroll
+    for (int k = 15; k >= 0; k--) {
+      if (k < bw) {
+        const float xk = readlane(acc * dj, k);
+        if (j == k) x = xk;
+        if (j < k) acc -= H[(c0 + k) * nv + c0 + j] * xk;
+      }
+    }
+    SYNC();
+    if (j < bw) dir[c0 + j] = x;
+    SYNC();
+    for (int r = j; r < c0; r += WAVE) {
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (k < bw) s += H[(c0 + k) * nv + r] * dir[c0 + k];
+      dir[r] -= s;
+    }
+    SYNC();
+  }
+}
+
 template <typename T, int NVM>
 __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const double* g, T* dir) {
   const int j = LANE;
@@ -2775,6 +2945,9 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       PMARK(PH_NCHOL);
     } else if (border_chol<T, DIM>() && !(M.dbg_flags & 1)) {
       if constexpr (border_chol<T, DIM>()) chol_sparse_border<DIM>(M, w, H, g, dir);
+      PMARK(PH_NCHOL);
+    } else if (dense_mfma_chol<T, DIM>() && !(M.dbg_flags & 3)) {
+      if constexpr (dense_mfma_chol<T, DIM>()) chol_dense_mfma<DIM>(w, H, nv, g, dir);
       PMARK(PH_NCHOL);
     } else if (!(M.dbg_flags & 1) && chol_sparse_lds(M, w, H, g, dir)) {
       PMARK(PH_NCHOL);

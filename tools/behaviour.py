@@ -54,6 +54,9 @@ def run_episodes(env, act_fn, want_per_arena, max_steps):
                 done_count[i] += 1
         if (done_count >= want_per_arena).all():
             break
+        if step % 50 == 49:  # progress on stderr (a long run otherwise looks hung)
+            print(f"step {step + 1}: {int((done_count >= want_per_arena).sum())}/{N} arenas done", file=sys.stderr,
+                  flush=True)
     return eps, int(step + 1), int((done_count >= want_per_arena).sum())
 
 

@@ -3,7 +3,7 @@
 solver setting, one JSON line per trajectory (tests/parity_util.summary + the setting).
 
 usage: FACTORYSIM_LIB=path python tools/parity_sweep.py --prec fp32 [--tol 1e-9] [--tag name]
-           [--traj A,K,T,seed ...]        (default: 2,4,96,7  2,4,300,21  2,8,300,5  2,10,250,9)
+           [--traj A,K,T,seed[,EnvClass] ...]   (default: 2,4,96,7  2,4,300,21  2,8,300,5  2,10,250,9)
 Trajectories are cached as .npz under gpurun_out/traj/ (or $FM_TRAJ_CACHE: a cache made in the container travels
 with the tree) so several processes share one oracle rollout.
 """
@@ -23,9 +23,11 @@ import parity_util as pu  # noqa: E402
 from oracle import pyoracle as po  # noqa: E402  (checker)
 
 
-def load_traj(A, K, T, seed, cache=os.environ.get("FM_TRAJ_CACHE", os.path.join(ROOT, "gpurun_out", "traj"))):
+def load_traj(A, K, T, seed, env_class="AllFullRLProgressRewardEnv",
+              cache=os.environ.get("FM_TRAJ_CACHE", os.path.join(ROOT, "gpurun_out", "traj"))):
     os.makedirs(cache, exist_ok=True)
-    f = os.path.join(cache, f"traj_{A}_{K}_{T}_{seed}.npz")
+    tag = "" if env_class == "AllFullRLProgressRewardEnv" else "_" + env_class
+    f = os.path.join(cache, f"traj_{A}_{K}_{T}_{seed}{tag}.npz")
     if os.path.exists(f):
         z = np.load(f)
         meta = json.load(open(f[:-4] + ".json"))
@@ -34,7 +36,7 @@ def load_traj(A, K, T, seed, cache=os.environ.get("FM_TRAJ_CACHE", os.path.join(
             outs.append(dict(obs=z["obs"][s], reward=float(z["reward"][s]), term=bool(z["term"][s]),
                              info=meta["info"][s], dbl=z["dbl"][s], ints=z["ints"][s], rng=z["rng"][s]))
         return z["recs"], z["acts"], outs
-    recs, acts, outs = pu.rollout(po, A, K, T, seed_actions=seed)
+    recs, acts, outs = pu.rollout(po, A, K, T, seed_actions=seed, env_class=env_class)
     np.savez(f, recs=recs, acts=acts, obs=np.stack([o["obs"] for o in outs]),
              reward=np.array([o["reward"] for o in outs]), term=np.array([o["term"] for o in outs]),
              dbl=np.stack([o["dbl"] for o in outs]), ints=np.stack([o["ints"] for o in outs]),
@@ -53,11 +55,13 @@ def main():
     args = ap.parse_args()
     po.build()
     for spec in args.traj:
-        A, K, T, seed = (int(x) for x in spec.split(","))
+        f = spec.split(",")
+        A, K, T, seed = (int(x) for x in f[:4])
+        env_class = f[4] if len(f) > 4 else "AllFullRLProgressRewardEnv"
         t0 = time.time()
-        traj = load_traj(A, K, T, seed)
+        traj = load_traj(A, K, T, seed, env_class)
         t1 = time.time()
-        r = pu.compare(traj, args.prec, A, K, solver_tolerance=args.tol, solver_iterations=args.iters)
+        r = pu.compare(traj, args.prec, A, K, env_class, solver_tolerance=args.tol, solver_iterations=args.iters)
         s = pu.summary(r)
         s.update(tag=args.tag, lib=os.path.basename(os.environ.get("FACTORYSIM_LIB", "libfactorysim.so")),
                  prec=args.prec, tol=args.tol,
