@@ -858,20 +858,20 @@ int fm_profile(fm_handle* h, int mode, uint64_t* host_out) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
   if (!h->prof) {
-    HIPCHK(hipMalloc((void**)&h->prof, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&h->prof, FM_NPROF * sizeof(unsigned long long)));
     h->allocs.push_back(h->prof);
-    HIPCHK(hipMemset(h->prof, 0, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(h->prof, 0, FM_NPROF * sizeof(unsigned long long)));
   }
   if (host_out) {
     HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemcpy(host_out, h->prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(host_out, h->prof, FM_NPROF * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     int khz = 0;
     HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
-    host_out[15] = (uint64_t)khz;
+    host_out[PH_KHZ] = (uint64_t)khz;
   }
   if (mode == 1) {
     HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemset(h->prof, 0, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(h->prof, 0, FM_NPROF * sizeof(unsigned long long)));
     h->prof_on = true;
   } else if (mode == 0) {
     h->prof_on = false;

@@ -217,7 +217,7 @@ struct Lay {
   int sort;   // int [K]
   int uctl;   // double [nu]  clipped control of this env-step
   int scal;   // double [4]   per-step scalars broadcast from lane 0
-  int prof;   // uint64 [16]  phase clocks of this arena (profiling only)
+  int prof;   // uint64 [FM_NPROF]  phase clocks of this arena (profiling only)
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
@@ -258,8 +258,10 @@ __host__ __device__ __forceinline__ const double* dslot(const T* rec, int k) {
   return (const double*)(rec + k);
 }
 // phase slots of the optional wall-clock profile (fm_profile)
+// (slot PH_KHZ is the host's clock rate; PH_CBOUND .. PH_CNARROW split the collision phase: geom centres and body
+// bounds, the body-pair midphase, the geom-pair expansion + narrowphase; PH_COLL keeps the contact ranking)
 enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_NHESS, PH_NCHOL, PH_NSOLVE, PH_NLS,
-       PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_LAST };
+       PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_KHZ, PH_CBOUND, PH_CMID, PH_CNARROW, PH_LAST = 23, FM_NPROF = 24 };
 enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE, MISC_CSUM,
        MISC_CMAX };
 // per-arena int64 counters (fm_get_counters): contacts dropped for capacity, Newton iterations, Newton
@@ -509,7 +511,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.sort = take(4 * K);
   L.uctl = take(8 * nu);
   L.scal = take(8 * 4);
-  L.prof = take(8 * 16);
+  L.prof = take(8 * FM_NPROF);
   L.total = off;
   if (spill) {  // the two largest arrays in the arena's global scratch block (L2 / HBM) instead of LDS
     L.spill = 1;

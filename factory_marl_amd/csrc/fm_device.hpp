@@ -1038,6 +1038,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   }
   if (LANE == 0) misc[MISC_NSTAGE] = 0;
   SYNC();
+  PMARK(PH_CBOUND);
   // 3. midphase: every allowed body pair's bounding test; the hits are compacted into sp[] (body pair | first
   // geom-pair index << 16) in one sweep, so the geom-pair expansion below runs over all of them at once
   uint32_t* sp = w.sp();
@@ -1083,6 +1084,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // pair-class -> params table, one entry per lane (read back with ds_bpermute, no memory access)
   const int ptab_l = LANE < 25 ? M.ptab[LANE] : 0;
   SYNC();
+  PMARK(PH_CMID);
   // 4. geom pairs of the hit body pairs, 64 per pass: bounding-sphere test, then binned by narrowphase cost:
   // box-box pairs (SAT + face clipping) in gsb, everything else (sphere-box, sphere-sphere, plane-*) in gs,
   // so a batch of 64 lanes runs one code path instead of the union of all of them
@@ -1159,6 +1161,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
   if (nbb > 0) narrow_batch(M, w, gsb, nbb);
   SYNC();
+  PMARK(PH_CNARROW);
   // 5. sort the staged contacts by key into the contact slots
   const int nst = misc[MISC_NSTAGE];
   const int ncon = nst < dm.maxcon ? nst : dm.maxcon;
@@ -3806,7 +3809,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   // a fresh opaque LDS base per use: workspace addresses are recomputed inside each phase instead of
   // being hoisted out of the substep loop (which would keep every phase's addresses live everywhere)
 #define w (Ws<T, DIM>{lds_base(smem), &L, spill_base<DIM>(S, arena)})
-  if (M.prof && LANE < 16) w.prof()[LANE] = LANE == PH_LAST ? wall_clock64() : 0ull;
+  if (M.prof && LANE < FM_NPROF) w.prof()[LANE] = LANE == PH_LAST ? wall_clock64() : 0ull;
   if (LANE == 0) {
     w.misc()[MISC_CSUM] = 0;
     w.misc()[MISC_CMAX] = 0;

@@ -460,16 +460,16 @@ class FactoryVecEnv:
 
     PHASES = ["fk", "geoms_mass", "collision", "rows", "smooth_acc", "newton_setup", "newton_grad",
               "newton_hessian", "newton_chol", "newton_solve", "newton_linesearch", "newton_final",
-              "integrate", "task_obs"]
+              "integrate", "task_obs", None, None, "coll_bounds", "coll_midphase", "coll_narrow"]
 
     def profile(self, mode=-1):
         """diagnostic phase profile (fm_profile): mode 1 zero+enable, 0 disable; returns
         ({phase: seconds summed over arenas}, ncon summed over stages)"""
         self._bind_stream()
-        out = np.zeros(16, np.uint64)
+        out = np.zeros(24, np.uint64)
         _lib.check(self._L.fm_profile(self._h, int(mode), out.ctypes.data_as(C.c_void_p)))
         khz = float(out[15]) or 1.0
-        return {p: float(out[i]) / (khz * 1e3) for i, p in enumerate(self.PHASES)}, int(out[14])
+        return {p: float(out[i]) / (khz * 1e3) for i, p in enumerate(self.PHASES) if p}, int(out[14])
 
     def debug_dump(self, arena=0, actuated=True):
         """diagnostic: internals of one recomputed physics stage (see fm_debug_dump)"""

@@ -151,11 +151,12 @@ int fm_set_state(fm_handle* h, const void* host_in);
  * cut), [6] objects in scene summed over env-steps, [7] episodes ended (terminations). */
 int fm_get_counters(fm_handle* h, int64_t* host_out);
 
-/* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [16] uint64).
+/* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [24] uint64).
  * mode 1 = zero and enable, 0 = disable, -1 = leave as is; host_out (may be NULL) receives the
- * totals: [0..13] clock ticks per phase (FK, geoms+M, collision, constraint rows, smooth acc,
+ * totals: [0..13] clock ticks per phase (FK, geoms+M, collision's contact ranking, constraint rows, smooth acc,
  * Newton setup / gradient / Hessian / Cholesky / solve / line search / final forces, integration,
- * task+obs), [14] sum of ncon over stages, [15] the clock rate in kHz. */
+ * task+obs), [14] sum of ncon over stages, [15] the clock rate in kHz, [16..18] the rest of the collision phase:
+ * geom centres + body bounds, body-pair midphase, geom-pair expansion + narrowphase; [19..23] zero. */
 int fm_profile(fm_handle* h, int mode, uint64_t* host_out);
 
 /* Diagnostic (tests only): recompute one mj_step1 + acceleration stage of `arena` at its stored stage

@@ -20,15 +20,22 @@ def main():
     ap.add_argument("--arms", type=int, default=2)
     ap.add_argument("--objects", type=int, default=4)
     ap.add_argument("--preroll", type=int, default=200, help="desynchronising pre-roll (bench.preroll)")
+    ap.add_argument("--env-class", default="AllFullRLProgressRewardEnv")
     args = ap.parse_args()
     import torch
 
     from factory_marl_amd import FactoryVecEnv
     from factory_marl_amd.environments import run_kwargs
 
-    env = FactoryVecEnv(args.arenas, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=args.arms,
-                                                           max_num_objects=args.objects, seed=42),
-                        precision=args.precision)
+    env = FactoryVecEnv(args.arenas, env_class=args.env_class,
+                        env_kwargs=run_kwargs(args.env_class, num_arms=args.arms, max_num_objects=args.objects, seed=42),
+                        precision=args.precision, return_numpy=False)
+    toggles = args.env_class in ("PauseIKToggleEnv", "BackupIKToggleEnv")
+
+    def act():
+        u = torch.rand(args.arenas, env.act_dim, device=env.device, generator=g)
+        return (u < 0.5).float() if toggles else u * 2 - 1
+
     env.reset()
     import bench
 
@@ -36,12 +43,12 @@ def main():
     g = torch.Generator(device=env.device)
     g.manual_seed(0)
     for _ in range(5):
-        env.step_tensors(torch.rand(args.arenas, env.act_dim, device=env.device, generator=g) * 2 - 1)
+        env.step_tensors(act())
     env.sync()
     c0 = env.counters().sum(0)
     env.profile(1)
     for _ in range(args.steps):
-        env.step_tensors(torch.rand(args.arenas, env.act_dim, device=env.device, generator=g) * 2 - 1)
+        env.step_tensors(act())
     env.sync()
     ph, ncon = env.profile(0)
     c1 = env.counters().sum(0)
@@ -49,12 +56,15 @@ def main():
     sub = args.arenas * args.steps * 100
     rep = {k: {"share": round(v / tot, 4), "us_per_arena_substep": round(v / sub * 1e6, 3)} for k, v in ph.items()}
     rep["_total_us_per_arena_substep"] = round(tot / sub * 1e6, 3)
+    coll = sum(ph[k] for k in ("coll_bounds", "coll_midphase", "coll_narrow", "collision"))
+    rep["_collision_total_us_per_arena_substep"] = round(coll / sub * 1e6, 3)  # "collision" = the contact ranking
     rep["_mean_ncon"] = round(ncon / sub, 3)
     rep["_lds_bytes_per_arena"] = env._L.fm_workspace_bytes(env._h)
     rep["_newton_iters_per_substep"] = round(float(c1[1] - c0[1]) / sub, 3)
     rep["_mean_objects_in_scene"] = round(float(c1[6] - c0[6]) / (args.arenas * args.steps), 3)
     rep["_preroll"] = args.preroll
     rep["_scene"] = f"{args.arms}x{args.objects}"
+    rep["_env_class"] = args.env_class
     print(json.dumps(rep, indent=1))
 
 
