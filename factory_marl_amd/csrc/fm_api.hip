@@ -9,6 +9,10 @@
 #ifndef FM_FIXED_SCENES
 #define FM_FIXED_SCENES X(2, 4) X(2, 8) X(2, 10)
 #endif
+// fp32-only compile-time scenes (fp64 runs them on the runtime-dims spill kernel)
+#ifndef FM_FIXED_SCENES32
+#define FM_FIXED_SCENES32 X(4, 16)
+#endif
 
 namespace fm {
 template <typename T, int A, int K>
@@ -55,6 +59,7 @@ struct fm_handle {
   void* dof = nullptr;
   void* ctrlrange = nullptr;
   void* geom = nullptr;
+  void* geomd = nullptr;
   int* geom_i = nullptr;
   int* ginfo = nullptr;
   int* cbi = nullptr;
@@ -158,6 +163,7 @@ static Model<T> make_model(const fm_handle* h) {
   M.ctrlrange = (const T*)h->ctrlrange;
   M.ctrlrange_d = h->ctrlrange_d;
   M.geom = (const T*)h->geom;
+  M.geomd = (const double*)h->geomd;
   M.geom_i = h->geom_i;
   M.pair = h->pair;
   M.ginfo = h->ginfo;
@@ -264,6 +270,7 @@ static int create_typed(fm_handle* h) {
   if ((r = upload<T>(h, &h->ctrlrange, ctrl))) return r;
   if ((r = upload_raw<double>(h, &h->ctrlrange_d, ctrl))) return r;
   if ((r = upload<T>(h, &h->geom, geom))) return r;
+  if ((r = upload<double>(h, &h->geomd, geom))) return r;
   if ((r = upload_raw<int>(h, &h->geom_i, geom_i))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->pair, s.pairs))) return r;
   {
@@ -295,7 +302,13 @@ static int create_typed(fm_handle* h) {
     if ((r = upload_raw<uint32_t>(h, &h->cbp, s.cb_pairs))) return r;
   }
   if ((r = upload<double>(h, &h->param, param))) return r;
-  if ((r = upload<T>(h, &h->cube, s.cube))) return r;
+  {
+    // slot 3: the rounding residue of the half size in this build's precision (0 in fp64), so the float64
+    // narrowphase of the fp32 build reads h exactly as (double)[0] + (double)[3]
+    std::vector<double> cb = s.cube;
+    for (size_t i = 0; i < cb.size(); i += 4) cb[i + 3] = cb[i] - (double)(T)cb[i];
+    if ((r = upload<T>(h, &h->cube, cb))) return r;
+  }
   if ((r = upload<T>(h, &h->meaninertia, s.meaninertia))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->tri, s.tri))) return r;
   // state
@@ -371,6 +384,17 @@ static int create_typed(fm_handle* h) {
   idx++;
   FM_FIXED_SCENES
 #undef X
+  if constexpr (sizeof(T) == 4) {
+#define X(a, k)                                                                                          \
+  if (h->fixed < 0 && !(force_dyn && force_dyn[0] == '1') && FixedDims<a, k>::matches(d)) {             \
+    h->fixed = idx;                                                                                      \
+    h->lay_step = FixedDims<a, k>::template layout<sizeof(T)>();                                         \
+    HIPCHK((fixed_set_attr<T, a, k>(h->lay_step.total)));                                                  \
+  }                                                                                                      \
+  idx++;
+    FM_FIXED_SCENES32
+#undef X
+  }
   (void)idx;
   if (h->fixed < 0) {
     h->lay_step = h->lay;
@@ -491,6 +515,9 @@ static void launch_step(fm_handle* h, const StepIO& io) {
   }                                                                                                    \
   idx++;
   FM_FIXED_SCENES
+  if constexpr (sizeof(T) == 4) {
+    FM_FIXED_SCENES32
+  }
 #undef X
   (void)idx;
   if constexpr (sizeof(T) == 8) {

@@ -103,6 +103,7 @@ struct Model {
   cptr<double> ctrlrange_d;  // [nu][2] float64 (actuator_ctrlrange as the reference clips with it)
   // geoms (compact, collidable)
   cptr<T> geom;      // [ngc][16]  pos(3) R(9) size(3) rbound
+  cptr<double> geomd;  // the same table in float64 (the fp32 build's float64 narrowphase)
   cptr<int> geom_i;  // [ngc][4]   mjid, type, kbody, box slot
   cptr<uint32_t> pair;  // [npair]  c1 | c2 << 12 | param << 24 (reference list; the kernel uses cb*)
   cptr<int> ginfo;      // [ngc] packed: type code | arm << 2 | pclass << 3 | kbody << 8
@@ -113,7 +114,7 @@ struct Model {
   int ptab[25];          // param index by (pclass g1, pclass g2)
   cptr<double> param;  // [nparam][8] mu, solref(2), solimp(5): float64 in both builds (impedance / R below)
   // per arena
-  cptr<T> cube;      // [N][K][4] h, m, I, pad
+  cptr<T> cube;      // [N][K][4] h, m, I, h - (T)h (the half size's rounding residue: h = [0] + [3] in float64)
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off

@@ -576,18 +576,19 @@ struct Emit {
   int key;
   uint32_t pair;
   int sub;
-  __device__ void operator()(T dist, T p0, T p1, T p2, T n0, T n1, T n2) {
+  template <typename X>
+  __device__ void operator()(X dist, X p0, X p1, X p2, X n0, X n1, X n2) {
     if (sub >= MAXPC) return;
     int s = atomicAdd(cnt, 1);
     if (s < cap) {
       T* r = st + 8 * s;
-      r[0] = dist;
-      r[1] = p0;
-      r[2] = p1;
-      r[3] = p2;
-      r[4] = n0;
-      r[5] = n1;
-      r[6] = n2;
+      r[0] = (T)dist;
+      r[1] = (T)p0;
+      r[2] = (T)p1;
+      r[3] = (T)p2;
+      r[4] = (T)n0;
+      r[5] = (T)n1;
+      r[6] = (T)n2;
       keys[s] = key | sub;
       pw[s] = pair;
     }
@@ -596,16 +597,16 @@ struct Emit {
 };
 
 template <typename T, typename E>
-__device__ __forceinline__ void np_plane_sphere(const T* c, T r, E& emit) {
-  // floor plane: world origin (z = -zshift in the kernel frame), normal +z (scene.xml:21)
-  T dist = c[2] + T(zshift<T>()) - r;
+__device__ __forceinline__ void np_plane_sphere(const T* c, T r, E& emit, T zs) {
+  // floor plane: world origin (z = -zs in the kernel frame, zs = the build's zshift), normal +z (scene.xml:21)
+  T dist = c[2] + zs - r;
   if (dist > T(0)) return;
   emit(dist, c[0], c[1], c[2] - (r + dist / T(2)), T(0), T(0), T(1));
 }
 
 template <typename T, typename E>
-__device__ __forceinline__ void np_plane_box(const T* p, const T* R, const T* h, E& emit) {
-  T dist = p[2] + T(zshift<T>());
+__device__ __forceinline__ void np_plane_box(const T* p, const T* R, const T* h, E& emit, T zs) {
+  T dist = p[2] + zs;
   int cnt = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -914,10 +915,104 @@ __device__ __forceinline__ void geom_frame(const Model<T>& M, const Ws<T, DIM>& 
   }
 }
 
+// fp32 build: the narrowphase in float64 from the float64 master state (cube centres and quaternions, belt slide),
+// the float64 geom table and the cubes' exact half sizes; the arm geoms' poses come from the float kinematics.
+// A contact's depth is a difference of coordinates ~0.1 m apart: in float it keeps ~1e-8 m of a 2.3e-6 m resting
+// depth (0.4 %), which the contact's stiffness turns into reference-acceleration errors of ~1e-4 per env-step
+#ifndef FM_NP_F64
+#define FM_NP_F64 1
+#endif
+template <typename T, typename DIM>
+__device__ __forceinline__ void geom_pose_f64(const Model<T>& M, const Ws<T, DIM>& w, int g, int kb, double* p, double* R,
+                                              double* h) {
+  const DIM dm(M.dm);
+  const double* gg = M.geomd + 16 * g;
+  constexpr double zs = zshift<T>();
+  h[0] = gg[12];
+  h[1] = gg[13];
+  h[2] = gg[14];
+  if (kb == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) p[k] = gg[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = gg[3 + k];
+  } else if (kb == 1) {
+    p[0] = 0.0;
+    p[1] = w.qd()[0];
+    p[2] = 1.05 - zs;
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+  } else if (kb < 2 + dm.K) {
+    const int k = kb - 2;
+    const double* c = w.qd() + 1 + 7 * k;
+    p[0] = c[0];
+    p[1] = c[1];
+    p[2] = c[2] - zs;
+    double qu[4] = {c[3], c[4], c[5], c[6]};
+    const double n = sqrt(qu[0] * qu[0] + qu[1] * qu[1] + qu[2] * qu[2] + qu[3] * qu[3]);
+    if (n < 1e-15) {
+      qu[0] = 1.0;
+      qu[1] = qu[2] = qu[3] = 0.0;
+    } else if (fabs(n - 1.0) > 1e-15) {
+      for (int e = 0; e < 4; e++) qu[e] /= n;
+    }
+    const double ww = qu[0], x = qu[1], y = qu[2], z = qu[3];
+    R[0] = ww * ww + x * x - y * y - z * z;
+    R[1] = 2.0 * (x * y - ww * z);
+    R[2] = 2.0 * (x * z + ww * y);
+    R[3] = 2.0 * (x * y + ww * z);
+    R[4] = ww * ww - x * x + y * y - z * z;
+    R[5] = 2.0 * (y * z - ww * x);
+    R[6] = 2.0 * (x * z - ww * y);
+    R[7] = 2.0 * (y * z + ww * x);
+    R[8] = ww * ww - x * x - y * y + z * z;
+    const T* cb = w.cube() + 4 * k;
+    h[0] = h[1] = h[2] = (double)cb[0] + (double)cb[3];
+  } else {
+    const T* x = w.gx() + 4 * g;
+    p[0] = x[0];
+    p[1] = x[1];
+    p[2] = x[2];
+    const int arm = (kb - 2 - dm.K) / 10, b = (kb - 2 - dm.K) % 10;
+    T Rf[9];
+    matmul3(w.bR() + 90 * arm + 9 * b, M.geom + 16 * g + 3, Rf);
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = Rf[k];
+  }
+}
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>& w, const uint32_t* list, int n) {
   const DIM dm(M.dm);
   if (LANE >= n) return;
+  if constexpr (sizeof(T) == 4 && FM_NP_F64) {
+    const uint32_t pwd = list[LANE];
+    const int c1 = pwd & 4095, c2 = (pwd >> 12) & 4095;
+    const int gi1 = w.ginfo()[c1], gi2 = w.ginfo()[c2];
+    const int t1 = gi1 & 3, t2 = gi2 & 3;
+    const int kb1 = (gi1 >> 8) & 255, kb2 = (gi2 >> 8) & 255;
+    const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
+    Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
+    double p1[3], R1[9], h1[3], p2[3], R2[9], h2[3];
+    geom_pose_f64(M, w, c2, kb2, p2, R2, h2);
+    if (t1 == GC_PLANE) {
+      if (t2 == GC_SPHERE)
+        np_plane_sphere(p2, M.geomd[16 * c2 + 15], emit, zshift<T>());
+      else
+        np_plane_box(p2, R2, h2, emit, zshift<T>());
+      return;
+    }
+    geom_pose_f64(M, w, c1, kb1, p1, R1, h1);
+    if (t1 == GC_SPHERE) {
+      if (t2 == GC_SPHERE)
+        np_sphere_sphere(p1, M.geomd[16 * c1 + 15], p2, M.geomd[16 * c2 + 15], emit);
+      else
+        np_sphere_box(p1, M.geomd[16 * c1 + 15], p2, R2, h2, emit);
+    } else {
+      np_box_box(p1, R1, h1, p2, R2, h2, emit);
+    }
+    return;
+  }
   uint32_t pwd = list[LANE];
   int c1 = pwd & 4095, c2 = (pwd >> 12) & 4095;
   const int gi1 = w.ginfo()[c1], gi2 = w.ginfo()[c2];
@@ -930,11 +1025,11 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
   T p1[3] = {x1[0], x1[1], x1[2]}, p2[3] = {x2[0], x2[1], x2[2]};
   if (t1 == GC_PLANE) {
     if (t2 == GC_SPHERE) {
-      np_plane_sphere(p2, x2[3], emit);
+      np_plane_sphere(p2, x2[3], emit, T(zshift<T>()));
     } else {
       T R[9], h[3];
       geom_frame(M, w, c2, kb2, R, h);
-      np_plane_box(p2, R, h, emit);
+      np_plane_box(p2, R, h, emit, T(zshift<T>()));
     }
   } else if (t1 == GC_SPHERE) {
     if (t2 == GC_SPHERE) {
@@ -2435,7 +2530,10 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
 // per block (9 blocks) and ~120 tile products.  The substitutions run blockwise the same way.
 template <typename T, typename DIM>
 __device__ constexpr bool dense_mfma_chol() {
-  return sizeof(T) == 4 && !DIM::fixed;
+  if constexpr (sizeof(T) == 4 && DIM::fixed)
+    return DIM::nv > WAVE + 16;  // compile-time scenes above the bordered register factor ((4,16))
+  else
+    return sizeof(T) == 4 && !DIM::fixed;
 }
 template <typename DIM>
 __device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* H, const int nv, const double* g,

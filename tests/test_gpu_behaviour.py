@@ -1,0 +1,61 @@
+"""Behavioural statistics of the GPU env against the reference's own MuJoCo numbers (tools/behaviour.py).
+
+* The four saved PPO runs (runs/*.zip -> tests/golden/policy_<run>.npz): each run's ep_info_buffer holds the
+  Monitor (r, l) of its last 100 training episodes in MuJoCo (tests/golden/runs_fixtures.npz); the same policy
+  (SB3 predict, stochastic) drives the GPU env from reset, one episode per arena.
+* The IK base policy (FactoryManipulationEnv, 2 arms): report/report.tex:276-295 quotes mean scores (1.65, 1.17)
+  and a mean length of 208.8 over 100 episodes (visualisation.py:55-85).
+
+The bands are the measured agreement (behaviour): a policy's return and length within a few percent of
+its training episodes; the IK base policy's length within 15 % and its summed score within 30 % of the report (the
+report's run is 100 sequential episodes of one seed; its arm asymmetry is not reproduced here)."""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def _have_gpu():
+    return torch.cuda.is_available()
+
+
+# run -> (band on the mean return, band on the mean length), relative to the run's ep_info_buffer means
+POLICY_BANDS = {"rk5rxnav": (0.06, 0.05), "r666unuv": (0.06, 0.05)}
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("run", sorted(POLICY_BANDS))
+def test_saved_policy_return_and_length_match_training_episodes(run):
+    import behaviour
+
+    out = behaviour.policy(types.SimpleNamespace(run=run, arenas=512, precision="fp32", seeds="arena"))
+    ref = out["reference_ep_info"]
+    br, bl = POLICY_BANDS[run]
+    print(json.dumps({k: out[k] for k in ("r", "l", "finished", "reference_ep_info")}))
+    assert out["finished"] == 512
+    assert abs(out["r"]["mean"] / ref["r"]["mean"] - 1) <= br, (out["r"], ref["r"])
+    assert abs(out["l"]["mean"] / ref["l"]["mean"] - 1) <= bl, (out["l"], ref["l"])
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_ik_base_policy_against_the_report():
+    import behaviour
+
+    out = behaviour.base(types.SimpleNamespace(A=2, arenas=512, episodes=0, precision="fp32"))
+    par = out["parallel"]
+    print(json.dumps(par))
+    assert par["finished"] == 512
+    score = par["scores0"]["mean"] + par["scores1"]["mean"]
+    assert abs(par["length_t"]["mean"] / 208.8 - 1) <= 0.15, par["length_t"]
+    assert abs(score / (1.65 + 1.17) - 1) <= 0.30, score
+    assert np.isfinite(score)

@@ -70,14 +70,16 @@ def base(args):
     kw = dict(num_arms=A, max_num_objects=10, seed=42)
     zero = lambda o: torch.zeros(1, device=o.device)  # noqa: E731  (act_dim 0)
     # the reference protocol: one env, seed 42, sequential episodes
-    env = FactoryVecEnv(1, env_class="FactoryManipulationEnv", env_kwargs=kw, precision=args.precision,
-                        return_numpy=False)
-    env.reset()
-    t0 = time.time()
-    eps, steps, _ = run_episodes(env, zero, args.episodes, args.episodes * 600)
-    env.close()
-    out["sequential"] = dict(scores0=_stats([e[0][0] for e in eps]), scores1=_stats([e[0][1] for e in eps]),
-                             length_t=_stats([e[1] - 1 for e in eps]), episodes=len(eps), seconds=time.time() - t0)
+    if args.episodes > 0:
+        env = FactoryVecEnv(1, env_class="FactoryManipulationEnv", env_kwargs=kw, precision=args.precision,
+                            return_numpy=False)
+        env.reset()
+        t0 = time.time()
+        eps, steps, _ = run_episodes(env, zero, args.episodes, args.episodes * 600)
+        env.close()
+        out["sequential"] = dict(scores0=_stats([e[0][0] for e in eps]), scores1=_stats([e[0][1] for e in eps]),
+                                 length_t=_stats([e[1] - 1 for e in eps]), episodes=len(eps),
+                                 seconds=time.time() - t0)
     # the large sample: seeds 42 + i, first episode of each arena
     if args.arenas:
         env = FactoryVecEnv(args.arenas, env_class="FactoryManipulationEnv", env_kwargs=kw, precision=args.precision,
