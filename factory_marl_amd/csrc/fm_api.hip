@@ -180,6 +180,8 @@ static Model<T> make_model(const fm_handle* h) {
   M.prof = h->prof_on ? h->prof : nullptr;
   const char* cl = getenv("FM_CHOL_LDS");
   M.dbg_flags = (cl && cl[0] == '1') ? 1 : ((cl && cl[0] == '2') ? 2 : 0);
+  const char* sb = getenv("FM_SERIAL_BOXBOX");  // experiment switch: one lane per box-box pair throughout
+  if (sb && sb[0] == '1') M.dbg_flags |= 4;
   return M;
 }
 

@@ -119,7 +119,8 @@ struct Model {
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
   int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one
-                             // instead of the dense matrix-core one for runtime-dims fp32 (FM_CHOL_LDS=2)
+                             // instead of the dense matrix-core one for runtime-dims fp32 (FM_CHOL_LDS=2); bit 2 = the
+                             // serial box-box narrowphase (FM_SERIAL_BOXBOX=1)
 };
 
 template <typename T>
@@ -260,9 +261,11 @@ __host__ __device__ __forceinline__ const double* dslot(const T* rec, int k) {
 }
 // phase slots of the optional wall-clock profile (fm_profile)
 // (slot PH_KHZ is the host's clock rate; PH_CBOUND .. PH_CNARROW split the collision phase: geom centres and body
-// bounds, the body-pair midphase, the geom-pair expansion + narrowphase; PH_COLL keeps the contact ranking)
+// bounds, the body-pair midphase, the geom-pair expansion + narrowphase; PH_COLL keeps the contact ranking;
+// PH_CHDIAG .. PH_CHSOLVE split the dense blocked Cholesky: diagonal blocks, panels, trailing updates, substitutions)
 enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_NHESS, PH_NCHOL, PH_NSOLVE, PH_NLS,
-       PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_KHZ, PH_CBOUND, PH_CMID, PH_CNARROW, PH_LAST = 23, FM_NPROF = 24 };
+       PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_KHZ, PH_CBOUND, PH_CMID, PH_CNARROW, PH_CHDIAG, PH_CHPANEL, PH_CHTRAIL,
+       PH_CHSOLVE, PH_LAST = 23, FM_NPROF = 24 };
 enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE, MISC_CSUM,
        MISC_CMAX };
 // per-arena int64 counters (fm_get_counters): contacts dropped for capacity, Newton iterations, Newton

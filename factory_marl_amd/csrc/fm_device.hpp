@@ -716,49 +716,81 @@ __device__ __forceinline__ T spick(int i, T a, T b, T c) {
 // the incident face with the reference face, enumerated as (1) incident vertices inside the reference
 // rectangle, (2) reference corners inside the incident quad, (3) proper edge/side crossings, each kept
 // if it penetrates (same definition as oracle/collide.c).  Normal from box1 to box2.
+// one separating axis of the box-box SAT (ax 0-2: box1's axes, 3-5: box2's, 6-14: edge crossings A_i x B_j,
+// normalised; false for a near-parallel edge pair): overlap ov and signed centre distance sd along u
+template <typename T>
+__device__ __forceinline__ bool bb_axis(int ax, const V3<T> (&A)[3], const V3<T> (&B)[3], const T* h1, const T* h2,
+                                        const V3<T>& d, V3<T>& u, T& ov, T& sd) {
+  if (ax < 3) {
+    u = vpick(ax, A[0], A[1], A[2]);
+  } else if (ax < 6) {
+    u = vpick(ax - 3, B[0], B[1], B[2]);
+  } else {
+    const int i = (ax - 6) / 3, j = (ax - 6) % 3;
+    u = vcross(vpick(i, A[0], A[1], A[2]), vpick(j, B[0], B[1], B[2]));
+    T n = sqrt(vdot(u, u));
+    if (n < T(1e-6)) return false;
+    u = V3<T>{u.x / n, u.y / n, u.z / n};
+  }
+  T ra = h1[0] * fabs(vdot(u, A[0])) + h1[1] * fabs(vdot(u, A[1])) + h1[2] * fabs(vdot(u, A[2]));
+  T rb = h2[0] * fabs(vdot(u, B[0])) + h2[1] * fabs(vdot(u, B[1])) + h2[2] * fabs(vdot(u, B[2]));
+  sd = vdot(u, d);
+  ov = ra + rb - fabs(sd);
+  return true;
+}
+
+// the SAT's outcome: the best face axis (0-5) and the best edge axis (6-14, or -1)
+template <typename T>
+struct BBSat {
+  int face_id, edge_id;
+  V3<T> face_u, edge_u;
+  T face_s, edge_s, best_face, best_edge;
+};
+
+template <typename T, typename E>
+__device__ __forceinline__ void np_box_box_finish(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2,
+                                                  const T* h2, const BBSat<T>& sat, E& emit);
+
 template <typename T, typename E>
 __device__ __forceinline__ void np_box_box(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2,
                                            const T* h2, E& emit) {
   const V3<T> A[3] = {vcol(R1, 0), vcol(R1, 1), vcol(R1, 2)};
   const V3<T> B[3] = {vcol(R2, 0), vcol(R2, 1), vcol(R2, 2)};
-  const V3<T> P1{p1[0], p1[1], p1[2]}, P2{p2[0], p2[1], p2[2]};
-  const V3<T> d{P2.x - P1.x, P2.y - P1.y, P2.z - P1.z};
-  T best_face = T(1e30), best_edge = T(1e30);
-  int face_id = -1, edge_id = -1;
-  V3<T> face_u{0, 0, 0}, edge_u{0, 0, 0};
-  T face_s = 0, edge_s = 0;
+  const V3<T> d{p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  BBSat<T> sat{-1, -1, V3<T>{0, 0, 0}, V3<T>{0, 0, 0}, T(0), T(0), T(1e30), T(1e30)};
 #pragma unroll
   for (int ax = 0; ax < 15; ax++) {
     V3<T> u;
-    if (ax < 3) {
-      u = A[ax];
-    } else if (ax < 6) {
-      u = B[ax - 3];
-    } else {
-      u = vcross(A[(ax - 6) / 3], B[(ax - 6) % 3]);
-      T n = sqrt(vdot(u, u));
-      if (n < T(1e-6)) continue;
-      u = V3<T>{u.x / n, u.y / n, u.z / n};
-    }
-    T ra = h1[0] * fabs(vdot(u, A[0])) + h1[1] * fabs(vdot(u, A[1])) + h1[2] * fabs(vdot(u, A[2]));
-    T rb = h2[0] * fabs(vdot(u, B[0])) + h2[1] * fabs(vdot(u, B[1])) + h2[2] * fabs(vdot(u, B[2]));
-    T sd = vdot(u, d);
-    T ov = ra + rb - fabs(sd);
+    T ov, sd;
+    if (!bb_axis(ax, A, B, h1, h2, d, u, ov, sd)) continue;
     if (ov < T(0)) return;
     if (ax < 6) {
-      if (ov < best_face) {
-        best_face = ov;
-        face_id = ax;
-        face_u = u;
-        face_s = sd;
+      if (ov < sat.best_face) {
+        sat.best_face = ov;
+        sat.face_id = ax;
+        sat.face_u = u;
+        sat.face_s = sd;
       }
-    } else if (ov < best_edge) {
-      best_edge = ov;
-      edge_id = ax;
-      edge_u = u;
-      edge_s = sd;
+    } else if (ov < sat.best_edge) {
+      sat.best_edge = ov;
+      sat.edge_id = ax;
+      sat.edge_u = u;
+      sat.edge_s = sd;
     }
   }
+  np_box_box_finish(p1, R1, h1, p2, R2, h2, sat, emit);
+}
+
+template <typename T, typename E>
+__device__ __forceinline__ void np_box_box_finish(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2,
+                                                  const T* h2, const BBSat<T>& sat, E& emit) {
+  const V3<T> A[3] = {vcol(R1, 0), vcol(R1, 1), vcol(R1, 2)};
+  const V3<T> B[3] = {vcol(R2, 0), vcol(R2, 1), vcol(R2, 2)};
+  const V3<T> P1{p1[0], p1[1], p1[2]}, P2{p2[0], p2[1], p2[2]};
+  const int face_id = sat.face_id, edge_id = sat.edge_id;
+  const T best_face = sat.best_face, best_edge = sat.best_edge;
+  const V3<T> face_u = sat.face_u, edge_u = sat.edge_u;
+  const T face_s = sat.face_s, edge_s = sat.edge_s;
   if (edge_id >= 0 && best_edge < T(0.95) * best_face) {
     T sg = edge_s >= T(0) ? T(1) : T(-1);
     V3<T> n{edge_u.x * sg, edge_u.y * sg, edge_u.z * sg};
@@ -1047,6 +1079,87 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
   }
 }
 
+// box-box pairs with the SAT spread over the wave: 4 pairs per pass, lanes 16 p .. 16 p + 14 evaluate axis
+// LANE & 15 of pair p (bb_axis: the serial loop's arithmetic), the group's separation test by ballot, the best
+// face / edge axis by a DPP row minimum (first axis on ties, as the serial strict '<' keeps), the winner's axis and
+// distance fetched by ds_bpermute; lane 16 p then builds the contacts (np_box_box_finish).  A pass costs one axis
+// plus one clipping instead of 15 axes plus the clipping on one lane.
+template <int CTRL>
+__device__ __forceinline__ double dpp_row(double x) {
+  return dpp_f64<CTRL>(x, x);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float x) {
+  return dpp_f32<CTRL>(x, x);
+}
+template <typename NP, typename T, typename DIM>
+__device__ __forceinline__ void geom_pose_np(const Model<T>& M, const Ws<T, DIM>& w, int g, int kb, NP* p, NP* R,
+                                             NP* h) {
+  if constexpr (sizeof(T) == 4 && FM_NP_F64) {
+    geom_pose_f64(M, w, g, kb, p, R, h);
+  } else {
+    const T* x = w.gx() + 4 * g;
+    p[0] = x[0];
+    p[1] = x[1];
+    p[2] = x[2];
+    geom_frame(M, w, g, kb, R, h);
+  }
+}
+template <typename T, typename DIM>
+__device__ __forceinline__ void narrow_bb_parallel(const Model<T>& M, const Ws<T, DIM>& w, const uint32_t* list,
+                                                   int n) {
+  using NP = std::conditional_t<(sizeof(T) == 4 && FM_NP_F64 != 0), double, T>;
+  const DIM dm(M.dm);
+  const int grp = LANE >> 4, ax = LANE & 15;
+  const uint64_t gm = 0xFFFFull << (16 * grp);
+  for (int p0 = 0; p0 < n; p0 += 4) {
+    const int pi = p0 + grp;
+    const bool live = pi < n;
+    const uint32_t pwd = list[live ? pi : 0];
+    const int c1 = pwd & 4095, c2 = (pwd >> 12) & 4095;
+    const int kb1 = (w.ginfo()[c1] >> 8) & 255, kb2 = (w.ginfo()[c2] >> 8) & 255;
+    NP p1[3], R1[9], h1[3], p2[3], R2[9], h2[3];
+    geom_pose_np<NP>(M, w, c1, kb1, p1, R1, h1);
+    geom_pose_np<NP>(M, w, c2, kb2, p2, R2, h2);
+    const V3<NP> A[3] = {vcol(R1, 0), vcol(R1, 1), vcol(R1, 2)};
+    const V3<NP> B[3] = {vcol(R2, 0), vcol(R2, 1), vcol(R2, 2)};
+    const V3<NP> d{p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    V3<NP> u{0, 0, 0};
+    NP ov = 0, sd = 0;
+    bool valid = false;
+    if (live && ax < 15) valid = bb_axis(ax, A, B, h1, h2, d, u, ov, sd);
+    const bool sep = (__ballot(valid && ov < NP(0)) & gm) != 0ull;
+    const bool isf = valid && ax < 6, ise = valid && ax >= 6;
+    NP fo = isf ? ov : NP(1e30), eo = ise ? ov : NP(1e30);
+    fo = fmin(fo, dpp_row<0x121>(fo));  // row_ror:1, 2, 4, 8: every lane of the row holds the row minimum
+    fo = fmin(fo, dpp_row<0x122>(fo));
+    fo = fmin(fo, dpp_row<0x124>(fo));
+    fo = fmin(fo, dpp_row<0x128>(fo));
+    eo = fmin(eo, dpp_row<0x121>(eo));
+    eo = fmin(eo, dpp_row<0x122>(eo));
+    eo = fmin(eo, dpp_row<0x124>(eo));
+    eo = fmin(eo, dpp_row<0x128>(eo));
+    const uint64_t fb = __ballot(isf && ov == fo) & gm;
+    const uint64_t eb = __ballot(ise && ov == eo) & gm;
+    const int fl = fb ? __builtin_ctzll(fb) : 16 * grp;
+    const int el = eb ? __builtin_ctzll(eb) : 16 * grp;
+    BBSat<NP> sat;
+    sat.face_id = fl & 15;
+    sat.face_u = V3<NP>{__shfl(u.x, fl), __shfl(u.y, fl), __shfl(u.z, fl)};
+    sat.face_s = __shfl(sd, fl);
+    sat.best_face = fo;
+    sat.edge_id = eb ? (el & 15) : -1;
+    sat.edge_u = V3<NP>{__shfl(u.x, el), __shfl(u.y, el), __shfl(u.z, el)};
+    sat.edge_s = __shfl(sd, el);
+    sat.best_edge = eo;
+    if (live && ax == 0 && !sep) {
+      const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
+      Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
+      np_box_box_finish(p1, R1, h1, p2, R2, h2, sat, emit);
+    }
+  }
+}
+
 // midphase passes of 64 body pairs that cover every possible pair of a compile-time scene
 template <typename DIM>
 __device__ constexpr int body_pair_passes() {
@@ -1254,7 +1367,12 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     }
   }
   if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
-  if (nbb > 0) narrow_batch(M, w, gsb, nbb);
+  if (nbb > 0) {
+    if (nbb <= 8 && !(M.dbg_flags & 4))
+      narrow_bb_parallel(M, w, gsb, nbb);
+    else
+      narrow_batch(M, w, gsb, nbb);
+  }
   SYNC();
   PMARK(PH_CNARROW);
   // 5. sort the staged contacts by key into the contact slots
@@ -2536,8 +2654,8 @@ __device__ constexpr bool dense_mfma_chol() {
     return sizeof(T) == 4 && !DIM::fixed;
 }
 template <typename DIM>
-__device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* H, const int nv, const double* g,
-                                                float* dir) {
+__device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<float, DIM>& w, float* H, const int nv,
+                                                const double* g, float* dir) {
   const int j = LANE;
   const int nb = (nv + 15) >> 4;
   float* dinv = (float*)w.tmp();  // quad()'s scratch, dead until the line search
@@ -2580,6 +2698,7 @@ __device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* 
       dinv[c0 + j] = di;
     }
     SYNC();
+    PMARK(PH_CHDIAG);
     // ---- panel: rows below the block, one per lane
     for (int r = c0 + bw + j; r < nv; r += WAVE) {
       float x[16];
@@ -2601,6 +2720,7 @@ __device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* 
         if (k < bw) Hr[k] = x[k];
     }
     SYNC();
+    PMARK(PH_CHPANEL);
     // ---- trailing update, lower-triangle tiles (I >= J) of the rows after the block
     const int t0 = b + 1;
     const int nt = nb - t0;
@@ -2628,6 +2748,7 @@ __device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* 
       }
     }
     SYNC();
+    PMARK(PH_CHTRAIL);
   }
   // ---- forward substitution L y = -g (y in dir), block by block
   for (int r = j; r < nv; r += WAVE) dir[r] = (float)-g[r];
@@ -2686,6 +2807,7 @@ __device__ __forceinline__ void chol_dense_mfma(const Ws<float, DIM>& w, float* 
     }
     SYNC();
   }
+  PMARK(PH_CHSOLVE);
 }
 
 template <typename T, int NVM>
@@ -3048,7 +3170,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       if constexpr (border_chol<T, DIM>()) chol_sparse_border<DIM>(M, w, H, g, dir);
       PMARK(PH_NCHOL);
     } else if (dense_mfma_chol<T, DIM>() && !(M.dbg_flags & 3)) {
-      if constexpr (dense_mfma_chol<T, DIM>()) chol_dense_mfma<DIM>(w, H, nv, g, dir);
+      if constexpr (dense_mfma_chol<T, DIM>()) chol_dense_mfma<DIM>(M, w, H, nv, g, dir);
       PMARK(PH_NCHOL);
     } else if (!(M.dbg_flags & 1) && chol_sparse_lds(M, w, H, g, dir)) {
       PMARK(PH_NCHOL);

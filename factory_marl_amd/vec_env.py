@@ -460,7 +460,8 @@ class FactoryVecEnv:
 
     PHASES = ["fk", "geoms_mass", "collision", "rows", "smooth_acc", "newton_setup", "newton_grad",
               "newton_hessian", "newton_chol", "newton_solve", "newton_linesearch", "newton_final",
-              "integrate", "task_obs", None, None, "coll_bounds", "coll_midphase", "coll_narrow"]
+              "integrate", "task_obs", None, None, "coll_bounds", "coll_midphase", "coll_narrow",
+              "chol_diag", "chol_panel", "chol_trail", "chol_solve"]
 
     def profile(self, mode=-1):
         """diagnostic phase profile (fm_profile): mode 1 zero+enable, 0 disable; returns

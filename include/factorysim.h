@@ -156,7 +156,8 @@ int fm_get_counters(fm_handle* h, int64_t* host_out);
  * totals: [0..13] clock ticks per phase (FK, geoms+M, collision's contact ranking, constraint rows, smooth acc,
  * Newton setup / gradient / Hessian / Cholesky / solve / line search / final forces, integration,
  * task+obs), [14] sum of ncon over stages, [15] the clock rate in kHz, [16..18] the rest of the collision phase:
- * geom centres + body bounds, body-pair midphase, geom-pair expansion + narrowphase; [19..23] zero. */
+ * geom centres + body bounds, body-pair midphase, geom-pair expansion + narrowphase; [19..22] the dense blocked
+ * Cholesky's diagonal blocks, panels, trailing updates and substitutions (scenes above 80 dofs, else 0); [23] zero. */
 int fm_profile(fm_handle* h, int mode, uint64_t* host_out);
 
 /* Diagnostic (tests only): recompute one mj_step1 + acceleration stage of `arena` at its stored stage

@@ -58,6 +58,8 @@ def main():
     rep["_total_us_per_arena_substep"] = round(tot / sub * 1e6, 3)
     coll = sum(ph[k] for k in ("coll_bounds", "coll_midphase", "coll_narrow", "collision"))
     rep["_collision_total_us_per_arena_substep"] = round(coll / sub * 1e6, 3)  # "collision" = the contact ranking
+    chol = sum(ph[k] for k in ("newton_chol", "chol_diag", "chol_panel", "chol_trail", "chol_solve"))
+    rep["_cholesky_total_us_per_arena_substep"] = round(chol / sub * 1e6, 3)
     rep["_mean_ncon"] = round(ncon / sub, 3)
     rep["_lds_bytes_per_arena"] = env._L.fm_workspace_bytes(env._h)
     rep["_newton_iters_per_substep"] = round(float(c1[1] - c0[1]) / sub, 3)
