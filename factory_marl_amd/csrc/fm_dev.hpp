@@ -446,6 +446,12 @@ struct StepParams {
 // scene (FixedDims) every offset is a constant, so LDS accesses use immediate offsets off one
 // lane-address register instead of one address register per array.
 // ------------------------------------------------------------------------------------------------
+// row stride of the Newton Hessian in LDS: fp32 scenes above 80 dofs factor it with the dense blocked matrix-core
+// Cholesky, which wants whole 16 x 16 blocks (rows / columns padded to a multiple of 16: zero, diagonal 1)
+__host__ __device__ constexpr int hstride(int tsize, int nv) { return (tsize == 4 && nv > 80) ? ((nv + 15) & ~15) : nv; }
+// scratch floats after the padded Hessian (the dense Cholesky's inverse diagonal block)
+__host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4 && nv > 80) ? 256 : 0; }
+
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false) {
   Lay L{};
@@ -491,7 +497,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   // float64 vectors (gradient, M (a - as), scratch; live from the solve to the integration) are never live
   // together
   const int u0 = off;
-  if (!spill) L.H = take(tsize * nv * nv);
+  if (!spill) L.H = take(tsize * (hstride(tsize, nv) * hstride(tsize, nv) + hextra(tsize, nv)));
   L.g = take(8 * nv);
   L.Ma = take(8 * nv);
   L.tmp = take(8 * nv);

@@ -2245,6 +2245,9 @@ __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_
 //  * Tree-block sparsity: H couples two trees only through a contact between them.  The coupling graph (plus
 //    the fill-in of this elimination order) comes from the tree->contact masks; a pivot updates only the row
 //    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
+#ifndef FM_CHOL_REFINE
+#define FM_CHOL_REFINE 1  // fp32 register Cholesky: one float64-residual refinement of the Newton direction
+#endif
 template <typename T, typename DIM>
 __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
                                                T* dir) {
@@ -2325,23 +2328,45 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
       });
     }
   });
-  T acc = j < NV ? (T)-g[jo] : T(0);
-  T y = T(0);
+  // L L' x = rhs with the factor in registers (forward, then backward substitution)
+  auto solve = [&](T rhs) -> T {
+    T acc = rhs;
+    T y = T(0);
 #pragma unroll
-  for (int k = 0; k < NV; k++) {
-    const T yk = readlane(acc * dinv, k);
-    if (j == k) y = yk;
-    if (j > k) acc -= col[k] * yk;
-  }
-  T acc2 = y, x = T(0);
+    for (int k = 0; k < NV; k++) {
+      const T yk = readlane(acc * dinv, k);
+      if (j == k) y = yk;
+      if (j > k) acc -= col[k] * yk;
+    }
+    T acc2 = y, x = T(0);
 #pragma unroll
-  for (int k = NV - 1; k >= 0; k--) {
-    const T xk = readlane(acc2 * dinv, k);
-    if (j == k) x = xk;
-    if (j < k) acc2 -= col[k] * dinv * xk;
-  }
+    for (int k = NV - 1; k >= 0; k--) {
+      const T xk = readlane(acc2 * dinv, k);
+      if (j == k) x = xk;
+      if (j < k) acc2 -= col[k] * dinv * xk;
+    }
+    return x;
+  };
+  T x = solve(j < NV ? (T)-g[jo] : T(0));
   if (j < NV) dir[jo] = x;
   SYNC();
+  if constexpr (sizeof(T) == 4 && FM_CHOL_REFINE) {
+    // one step of iterative refinement: the residual of H x = -g in float64 (H is intact in LDS: the factor lives
+    // in registers), solved with the same factor.  The fp32 factor's error (~ nv eps cond(H)) otherwise stays in
+    // the Newton direction, and with MuJoCo's tolerance Newton stops after that one direction
+    double r = j < NV ? -g[jo] : 0.0;
+    if (j < NV) {
+#pragma unroll
+      for (int i = 0; i < NV; i++) {
+        const int io = i == NV - 1 ? 0 : i + 1;
+        r -= (double)H[jo * NV + io] * (double)dir[io];
+      }
+    }
+    SYNC();
+    x += solve((T)r);
+    if (j < NV) dir[jo] = x;
+    SYNC();
+  }
 }
 
 // fp32, compile-time scene with 64 < nv <= 80 ((2,8), (2,10)): the same register Cholesky for the 64 leading
@@ -2553,6 +2578,7 @@ template <typename T, typename DIM>
 __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, DIM>& w, T* H, const double* g, T* dir) {
   const DIM dm(M.dm);
   const int NV = dm.nv, K = dm.K, NT = dm.ntree, A0 = 1 + 6 * K;
+  const int HS = hstride(sizeof(T), NV);  // the Hessian's row stride
   if (NT > 32) return false;
   const int NW = (dm.maxcon + 63) / 64;
   T* dinv = (T*)w.tmp();      // quad()'s scratch, dead until the line search
@@ -2580,7 +2606,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
   for (int k = 0; k < NV; k++) {
     const int tk = tree_of(k), dk = dof(k);
     const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
-    T d = H[dk * NV + dk];
+    T d = H[dk * HS + dk];
     d = d > tiny ? d : tiny;
     const T ri = T(1) / sqrt(d);
     int m = 0;
@@ -2594,7 +2620,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
     }
     if (LANE == 0) dinv[k] = ri;
     SYNC();
-    for (int e = LANE; e < m; e += WAVE) H[dof(list[e]) * NV + dk] *= ri;  // L[i][k]
+    for (int e = LANE; e < m; e += WAVE) H[dof(list[e]) * HS + dk] *= ri;  // L[i][k]
     SYNC();
     // trailing update of the row set's lower triangle, one (row, column) pair per lane: the m (m + 1) / 2 pairs
     // are spread over the wave (a pair's entry is written by that lane only; column dk is read-only here)
@@ -2605,7 +2631,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
       if (a * (a + 1) / 2 > e) a--;
       const int b = e - a * (a + 1) / 2;
       const int di = dof(list[a]), dc = dof(list[b]);
-      H[di * NV + dc] -= H[di * NV + dk] * H[dc * NV + dk];
+      H[di * HS + dc] -= H[di * HS + dk] * H[dc * HS + dk];
     }
     SYNC();
   }
@@ -2620,7 +2646,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
     const T yk = dir[dk] * dinv[k];
     if (LANE == 0) yv[dk] = yk;
     for (int p = k + 1 + LANE; p < NV; p += WAVE)
-      if ((ak >> tree_of(p)) & 1u) dir[dof(p)] -= H[dof(p) * NV + dk] * yk;
+      if ((ak >> tree_of(p)) & 1u) dir[dof(p)] -= H[dof(p) * HS + dk] * yk;
     SYNC();
   }
   for (int k = NV - 1; k >= 0; k--) {  // L' x = y
@@ -2629,23 +2655,24 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
     const T xk = yv[dk] * dinv[k];
     if (LANE == 0) dir[dk] = xk;
     for (int p = LANE; p < k; p += WAVE)
-      if ((ak >> tree_of(p)) & 1u) yv[dof(p)] -= H[dk * NV + dof(p)] * xk;
+      if ((ak >> tree_of(p)) & 1u) yv[dof(p)] -= H[dk * HS + dof(p)] * xk;
     SYNC();
   }
   return true;
 }
 
-// fp32 runtime-dims scenes with nv > 64 ((4,16): 133 dofs): dense right-looking Cholesky over 16-wide column
-// blocks of H (LDS, row-major, original numbering; only the lower triangle is read or written), the trailing
-// update on the matrix cores.  Per block b (columns c0 .. c0 + 15):
-//  * the 16 x 16 diagonal block is factored in registers on lanes 0..15 (lane j owns row j; pivots broadcast by
-//    v_readlane), written back with the pivots' reciprocals;
-//  * the panel below it, L[r][blk] = H[r][blk] L_bb^-T, one row per lane (the L_bb entries are uniform LDS reads);
-//  * the trailing lower triangle H -= L_panel L_panel' tile by tile, one 16 x 16 tile = 4 chained
-//    v_mfma_f32_16x16x4_f32 whose A and B operands are panel entries (A[i][k] = L[16I + i][c0 + k],
-//    B[k][j] = L[16J + j][c0 + k]).
-// The sparse LDS path spends 3 wave barriers and a ballot compaction per pivot (133 pivots); this one spends 3
-// per block (9 blocks) and ~120 tile products.  The substitutions run blockwise the same way.
+// fp32 scenes above 80 dofs ((4,16): 133; compile-time or runtime dims): dense right-looking Cholesky over
+// 16-wide column blocks of H (LDS, row stride hs = nv rounded up to 16, padding an identity block; only the lower
+// triangle is read), everything but the 16-step pivot chains on the matrix cores.  Per block b (columns c0..c0+15):
+//  * the diagonal block is factored in registers (lane j < 16 owns row j; pivots broadcast by v_readlane) and
+//    inverted (lane j forms column j of L_bb^-1 by substitution; the entries of L_bb arrive by v_readlane);
+//  * the panel below it, P = H_panel L_bb^-T, one 16 x 16 tile = 4 chained v_mfma_f32_16x16x4_f32
+//    (A = H_panel, B = (L_bb^-1)^T);
+//  * the trailing lower triangle H -= P P' tile by tile, 4 MFMAs per tile (A[i][k] = P[16I + i][k],
+//    B[k][j] = P[16J + j][k]); diagonal tiles are written whole (their upper halves are never read).
+// The substitutions run blockwise: the 16-step chain on lanes 0..15, then one row per lane over the rest with the
+// block's solution broadcast by v_readlane.  Row / column operands are read unconditionally (the padding makes
+// every block whole), so the loads of a tile issue together.
 template <typename T, typename DIM>
 __device__ constexpr bool dense_mfma_chol() {
   if constexpr (sizeof(T) == 4 && DIM::fixed)
@@ -2656,126 +2683,162 @@ __device__ constexpr bool dense_mfma_chol() {
 template <typename DIM>
 __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<float, DIM>& w, float* H, const int nv,
                                                 const double* g, float* dir) {
-  const int j = LANE;
-  const int nb = (nv + 15) >> 4;
-  float* dinv = (float*)w.tmp();  // quad()'s scratch, dead until the line search
+  const int hs = hstride(4, nv);
+  const int nb = hs >> 4;
+  const int j = LANE, j16 = j & 15, q4 = j >> 4;
+  float* dinv = (float*)w.tmp();  // [hs] 1 / L_kk (quad()'s scratch, dead until the line search)
+  float* IL = H + hs * hs;        // [16][16] L_bb^-1 of the current block (hextra)
   const float tiny = 1e-37f;
   for (int b = 0; b < nb; b++) {
     const int c0 = 16 * b;
-    const int bw = nv - c0 < 16 ? nv - c0 : 16;
-    // ---- diagonal block: lane j < bw holds row c0 + j (lower entries at (max, min))
+    // ---- diagonal block: lane j16 holds row c0 + j16 (lower entries read at (max, min))
     float col[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      const int hi = i > j ? i : j, lo = i > j ? j : i;
-      col[i] = (j < bw && i < bw) ? H[(c0 + hi) * nv + c0 + lo] : 0.0f;
+      const int hi = i > j16 ? i : j16, lo = i > j16 ? j16 : i;
+      col[i] = H[(c0 + hi) * hs + c0 + lo];
     }
     float di = 1.0f;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      if (k < bw) {
-        float d = readlane(col[k], k);
-        d = d > tiny ? d : tiny;
-        const float ri = 1.0f / sqrtf(d);
-        const float lj = col[k] * ri;  // lane j > k: L[j][k]; lane k: L[k][k]
-        if (j == k) di = ri;
-        if (j >= k) col[k] = lj;
-        if (j > k) {
-          float lv[16];
+      float d = readlane(col[k], k);
+      d = d > tiny ? d : tiny;
+      const float ri = 1.0f / sqrtf(d);
+      const float lj = col[k] * ri;  // lane j16 > k: L[j16][k]; lane k: L[k][k]
+      if (j16 == k) di = ri;
+      if (j16 >= k) col[k] = lj;
+      float lv[16];
 #pragma unroll
-          for (int i = 0; i < 16; i++) lv[i] = i > k ? readlane(lj, i) : 0.0f;
+      for (int i = 0; i < 16; i++) lv[i] = i > k ? readlane(lj, i) : 0.0f;
+      if (j16 > k) {
 #pragma unroll
-          for (int i = 0; i < 16; i++)
-            if (i > k) col[i] -= lv[i] * lj;
-        }
+        for (int i = 0; i < 16; i++)
+          if (i > k) col[i] -= lv[i] * lj;
       }
     }
-    SYNC();  // every lane has read its block before it is overwritten
-    if (j < bw) {
+    // ---- L_bb^-1, column j16 on lane j16: z_i = (delta_ij - sum_{m<i} L[i][m] z_m) / L_ii
+    float z[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      float sacc = i == j16 ? 1.0f : 0.0f;
+#pragma unroll
+      for (int m = 0; m < i; m++) sacc -= readlane(col[m], i) * z[m];
+      z[i] = sacc * readlane(di, i);
+    }
+    SYNC();  // every lane has read its block
+    if (j < 16) {
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        if (k <= j) H[(c0 + j) * nv + c0 + k] = col[k];
+        if (k <= j) H[(c0 + j) * hs + c0 + k] = col[k];
+#pragma unroll
+      for (int i = 0; i < 16; i++) IL[16 * i + j] = z[i];
       dinv[c0 + j] = di;
     }
     SYNC();
     PMARK(PH_CHDIAG);
-    // ---- panel: rows below the block, one per lane
-    for (int r = c0 + bw + j; r < nv; r += WAVE) {
-      float x[16];
-      float* Hr = H + r * nv + c0;
+    // ---- panel: P = H_panel L_bb^-T, tile rows below the block
+    {
+      float bo[4];
 #pragma unroll
-      for (int k = 0; k < 16; k++) x[k] = k < bw ? Hr[k] : 0.0f;
+      for (int s = 0; s < 4; s++) bo[s] = IL[16 * j16 + 4 * s + q4];  // B[k][jj] = L^-1[jj][k]
+      for (int rI = c0 + 16; rI < hs; rI += 16) {
+        float a[4];
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
-        if (k < bw) {
-          float s = x[k];
-          const float* Lk = H + (c0 + k) * nv + c0;
+        for (int s = 0; s < 4; s++) a[s] = H[(rI + j16) * hs + c0 + 4 * s + q4];
+        fm_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int m = 0; m < k; m++) s -= x[m] * Lk[m];
-          x[k] = s * dinv[c0 + k];
-        }
+        for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[s], acc, 0, 0, 0);
+        SYNC();  // the tile's reads before its writes (other lanes read the same rows)
+#pragma unroll
+        for (int r = 0; r < 4; r++) H[(rI + 4 * q4 + r) * hs + c0 + j16] = acc[r];
       }
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        if (k < bw) Hr[k] = x[k];
     }
     SYNC();
     PMARK(PH_CHPANEL);
-    // ---- trailing update, lower-triangle tiles (I >= J) of the rows after the block
-    const int t0 = b + 1;
-    const int nt = nb - t0;
-    const int ntile = nt * (nt + 1) / 2;
-    const int li = j & 15, lk = j >> 4;
-    for (int t = 0; t < ntile; t++) {
-      int I = 0;
-      while ((I + 1) * (I + 2) / 2 <= t) I++;
-      const int J = t - I * (I + 1) / 2;
-      const int rI = 16 * (t0 + I), rJ = 16 * (t0 + J);
-      fm_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // ---- trailing update of the lower-triangle tiles (I >= J) after the block, two tiles per pass
+    {
+      const int t0 = b + 1;
+      const int nt = nb - t0;
+      const int ntile = nt * (nt + 1) / 2;
+      int I = 0, J = 0;  // tile t -> (I, J), walked incrementally
+      for (int t = 0; t < ntile; t += 2) {
+        const int I1 = I, J1 = J;
+        int I2 = I1, J2 = J1 + 1;
+        if (J2 > I2) {
+          I2++;
+          J2 = 0;
+        }
+        const bool two = t + 1 < ntile;
+        const int rI1 = 16 * (t0 + I1), rJ1 = 16 * (t0 + J1);
+        const int rI2 = 16 * (t0 + (two ? I2 : I1)), rJ2 = 16 * (t0 + (two ? J2 : J1));
+        float a1[4], b1[4], a2[4], b2[4];
 #pragma unroll
-      for (int s = 0; s < 4; s++) {
-        const int c = c0 + 4 * s + lk;
-        const bool cok = c < c0 + bw;
-        const float a = (cok && rI + li < nv) ? H[(rI + li) * nv + c] : 0.0f;
-        const float bb = (cok && rJ + li < nv) ? H[(rJ + li) * nv + c] : 0.0f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
-      }
-      const int cc = rJ + li;
+        for (int s = 0; s < 4; s++) {
+          const int c = c0 + 4 * s + q4;
+          a1[s] = H[(rI1 + j16) * hs + c];
+          b1[s] = H[(rJ1 + j16) * hs + c];
+          a2[s] = H[(rI2 + j16) * hs + c];
+          b2[s] = H[(rJ2 + j16) * hs + c];
+        }
+        float c1[4], c2[4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int rr = rI + 4 * lk + q;
-        if (rr < nv && cc < nv && rr >= cc) H[rr * nv + cc] -= acc[q];
+        for (int r = 0; r < 4; r++) {
+          c1[r] = H[(rI1 + 4 * q4 + r) * hs + rJ1 + j16];
+          c2[r] = H[(rI2 + 4 * q4 + r) * hs + rJ2 + j16];
+        }
+        fm_f32x4 acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b1[s], acc1, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[s], b2[s], acc2, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) H[(rI1 + 4 * q4 + r) * hs + rJ1 + j16] = c1[r] - acc1[r];
+        if (two) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) H[(rI2 + 4 * q4 + r) * hs + rJ2 + j16] = c2[r] - acc2[r];
+        }
+        I = I2;
+        J = J2 + 1;
+        if (J > I) {
+          I++;
+          J = 0;
+        }
       }
     }
     SYNC();
     PMARK(PH_CHTRAIL);
   }
-  // ---- forward substitution L y = -g (y in dir), block by block
+  // ---- forward substitution L y = -g (y in dir; padded rows stay 0 and are never stored)
   for (int r = j; r < nv; r += WAVE) dir[r] = (float)-g[r];
   SYNC();
   for (int b = 0; b < nb; b++) {
     const int c0 = 16 * b;
-    const int bw = nv - c0 < 16 ? nv - c0 : 16;
-    float acc = j < bw ? dir[c0 + j] : 0.0f;
-    const float dj = j < bw ? dinv[c0 + j] : 1.0f;
+    float lrow[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) lrow[k] = H[(c0 + j16) * hs + c0 + k];
+    const bool own = j < 16 && c0 + j < nv;
+    float acc = own ? dir[c0 + j] : 0.0f;
+    const float dj = dinv[c0 + j16];
     float y = 0.0f;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      if (k < bw) {
-        const float yk = readlane(acc * dj, k);
-        if (j == k) y = yk;
-        if (j > k && j < bw) acc -= H[(c0 + j) * nv + c0 + k] * yk;
-      }
+      const float yk = readlane(acc * dj, k);
+      if (j16 == k) y = yk;
+      if (j16 > k) acc -= lrow[k] * yk;
     }
+    float yb[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) yb[k] = readlane(y, k);
     SYNC();
-    if (j < bw) dir[c0 + j] = y;
-    SYNC();
-    for (int r = c0 + bw + j; r < nv; r += WAVE) {
-      const float* Lr = H + r * nv + c0;
+    if (own) dir[c0 + j] = y;
+    for (int r = c0 + 16 + j; r < nv; r += WAVE) {
+      float lr[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) lr[k] = H[r * hs + c0 + k];
       float s = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 16; k++)
-        if (k < bw) s += Lr[k] * dir[c0 + k];
+      for (int k = 0; k < 16; k++) s += lr[k] * yb[k];
       dir[r] -= s;
     }
     SYNC();
@@ -2783,26 +2846,31 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
   // ---- backward substitution L' x = y, last block first
   for (int b = nb - 1; b >= 0; b--) {
     const int c0 = 16 * b;
-    const int bw = nv - c0 < 16 ? nv - c0 : 16;
-    float acc = j < bw ? dir[c0 + j] : 0.0f;
-    const float dj = j < bw ? dinv[c0 + j] : 1.0f;
+    float lcol[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) lcol[k] = H[(c0 + (k > j16 ? k : j16)) * hs + c0 + (k > j16 ? j16 : k)];
+    const bool own = j < 16 && c0 + j < nv;
+    float acc = own ? dir[c0 + j] : 0.0f;
+    const float dj = dinv[c0 + j16];
     float x = 0.0f;
 #pragma unroll
     for (int k = 15; k >= 0; k--) {
-      if (k < bw) {
-        const float xk = readlane(acc * dj, k);
-        if (j == k) x = xk;
-        if (j < k) acc -= H[(c0 + k) * nv + c0 + j] * xk;
-      }
+      const float xk = readlane(acc * dj, k);
+      if (j16 == k) x = xk;
+      if (j16 < k) acc -= lcol[k] * xk;
     }
+    float xb[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) xb[k] = readlane(x, k);
     SYNC();
-    if (j < bw) dir[c0 + j] = x;
-    SYNC();
+    if (own) dir[c0 + j] = x;
     for (int r = j; r < c0; r += WAVE) {
+      float lc[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) lc[k] = H[(c0 + k) * hs + r];
       float s = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 16; k++)
-        if (k < bw) s += H[(c0 + k) * nv + r] * dir[c0 + k];
+      for (int k = 0; k < 16; k++) s += lc[k] * xb[k];
       dir[r] -= s;
     }
     SYNC();
@@ -3035,6 +3103,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   double* Ma = w.Ma();
   double* tmp = w.tmp();
   T* H = w.H();
+  const int hs = hstride(sizeof(T), nv);  // == nv except for the dense blocked Cholesky's scenes
   const double scale = 1.0 / ((double)M.meaninertia[arena] * (double)(nv > 1 ? nv : 1));
   const double tol = M.solver_tol;
   // quadratic part helper: returns 1/2 (x-as)' M (x-as), leaves M(x-as) in Ma
@@ -3084,20 +3153,22 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     {
       // zero fill in 16-byte stores (the region is 16-byte aligned), then the tail
       constexpr int PER16 = 16 / sizeof(T);
-      const int n16 = nv * nv / PER16;
+      const int n16 = hs * hs / PER16;
       uint4* H16 = (uint4*)H;
       for (int e = LANE; e < n16; e += WAVE) H16[e] = make_uint4(0u, 0u, 0u, 0u);
-      for (int e = n16 * PER16 + LANE; e < nv * nv; e += WAVE) H[e] = T(0);
+      for (int e = n16 * PER16 + LANE; e < hs * hs; e += WAVE) H[e] = T(0);
     }
     SYNC();
     {
       int a0 = 1 + 6 * dm.K;
-      for (int i = LANE; i < nv; i += WAVE) {
-        if (i < a0) {
-          H[i * nv + i] = Mdiag(M, w, i);
+      for (int i = LANE; i < hs; i += WAVE) {
+        if (i >= nv) {
+          H[i * hs + i] = T(1);  // padding (dense blocked Cholesky): an identity block
+        } else if (i < a0) {
+          H[i * hs + i] = Mdiag(M, w, i);
         } else {
           int arm = (i - a0) / 9, r = (i - a0) % 9;
-          for (int j = 0; j < 9; j++) H[i * nv + a0 + 9 * arm + j] = w.Marm()[81 * arm + 9 * r + j];
+          for (int j = 0; j < 9; j++) H[i * hs + a0 + 9 * arm + j] = w.Marm()[81 * arm + 9 * r + j];
         }
       }
     }
@@ -3125,7 +3196,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       const T q2 = Kc[4] * b0 + Kc[5] * b1 + Kc[2] * b2;
       const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
       const int gi = ii < nda ? oa + ii : ob + ii - nda;
-      T* Hrow = H + gi * nv;
+      T* Hrow = H + gi * hs;
       T jr0[CJ], jr1[CJ], jr2[CJ];
 #pragma unroll
       for (int jj = 0; jj < CJ; jj++) {
@@ -3148,11 +3219,11 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       if (!(ri[2] == 0 || *dslot(rr, RR_JAR) < 0.0)) continue;
       const T D = rr[RR_D];
       const int d0 = ri[0], d1 = ri[1];
-      atomicAdd(H + d0 * nv + d0, D * rr[RR_C0] * rr[RR_C0]);
+      atomicAdd(H + d0 * hs + d0, D * rr[RR_C0] * rr[RR_C0]);
       if (d1 >= 0) {
-        atomicAdd(H + d1 * nv + d1, D * rr[RR_C1] * rr[RR_C1]);
-        atomicAdd(H + d0 * nv + d1, D * rr[RR_C0] * rr[RR_C1]);
-        atomicAdd(H + d1 * nv + d0, D * rr[RR_C0] * rr[RR_C1]);
+        atomicAdd(H + d1 * hs + d1, D * rr[RR_C1] * rr[RR_C1]);
+        atomicAdd(H + d0 * hs + d1, D * rr[RR_C0] * rr[RR_C1]);
+        atomicAdd(H + d1 * hs + d0, D * rr[RR_C0] * rr[RR_C1]);
       }
     }
     SYNC();
@@ -3169,7 +3240,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     } else if (border_chol<T, DIM>() && !(M.dbg_flags & 1)) {
       if constexpr (border_chol<T, DIM>()) chol_sparse_border<DIM>(M, w, H, g, dir);
       PMARK(PH_NCHOL);
-    } else if (dense_mfma_chol<T, DIM>() && !(M.dbg_flags & 3)) {
+    } else if (dense_mfma_chol<T, DIM>() && nv > 80 && !(M.dbg_flags & 3)) {  // hstride() pads these
       if constexpr (dense_mfma_chol<T, DIM>()) chol_dense_mfma<DIM>(M, w, H, nv, g, dir);
       PMARK(PH_NCHOL);
     } else if (!(M.dbg_flags & 1) && chol_sparse_lds(M, w, H, g, dir)) {
@@ -3179,18 +3250,18 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       int colstart = 0;
       for (int k = 0; k < nv; k++) {
         if (LANE == 0) {
-          T s = H[k * nv + k];
-          H[k * nv + k] = sqrt(s > T(1e-300) ? s : T(1e-300));
+          T s = H[k * hs + k];
+          H[k * hs + k] = sqrt(s > T(1e-300) ? s : T(1e-300));
         }
         SYNC();
-        T lkk = H[k * nv + k];
-        for (int i = k + 1 + LANE; i < nv; i += WAVE) H[i * nv + k] /= lkk;
+        T lkk = H[k * hs + k];
+        for (int i = k + 1 + LANE; i < nv; i += WAVE) H[i * hs + k] /= lkk;
         SYNC();
         colstart += nv - k;  // start of column k+1 in the table
         for (int e = colstart + LANE; e < ntri; e += WAVE) {
           uint32_t ij = M.tri[e];
           int i = ij & 0xFFFF, j = ij >> 16;
-          H[i * nv + j] -= H[i * nv + k] * H[j * nv + k];
+          H[i * hs + j] -= H[i * hs + k] * H[j * hs + k];
         }
         SYNC();
       }
@@ -3199,17 +3270,17 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       for (int i = LANE; i < nv; i += WAVE) dir[i] = (T)-g[i];
       SYNC();
       for (int k = 0; k < nv; k++) {
-        T xk = dir[k] / H[k * nv + k];
+        T xk = dir[k] / H[k * hs + k];
         SYNC();
         if (LANE == 0) dir[k] = xk;
-        for (int i = k + 1 + LANE; i < nv; i += WAVE) dir[i] -= H[i * nv + k] * xk;
+        for (int i = k + 1 + LANE; i < nv; i += WAVE) dir[i] -= H[i * hs + k] * xk;
         SYNC();
       }
       for (int k = nv - 1; k >= 0; k--) {
-        T xk = dir[k] / H[k * nv + k];
+        T xk = dir[k] / H[k * hs + k];
         SYNC();
         if (LANE == 0) dir[k] = xk;
-        for (int i = LANE; i < k; i += WAVE) dir[i] -= H[k * nv + i] * xk;
+        for (int i = LANE; i < k; i += WAVE) dir[i] -= H[k * hs + i] * xk;
         SYNC();
       }
     }

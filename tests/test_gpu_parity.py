@@ -87,14 +87,17 @@ def test_teacher_forced_fp32(trajectory, long_trajectory, which):
           f"median {np.median(e):.2e}, worst {e.max():.2e}; integer/flag divergences "
           f"{len(r['int_bad'])}/{len(r['flag_bad'])}; obs worst {r['obs_err'].max():.2e}; "
           f"missing steps {list(r['err_steps'][e > 1e-4])}")
-    assert len(r["flag_bad"]) + len(r["int_bad"]) <= 0.01 * len(e), (r["flag_bad"], r["int_bad"])
-    # fp32 physics over a float64 master state in a z-shifted frame: measured 95.8 % (96 steps)
-    # and 94.6-95.2 % (300 steps, median 1.1e-5 - 2.2e-5).  The misses are the landing impacts of freshly
-    # spawned cubes (env-steps 4-5, 52-53, 97 after each reset, in every trajectory) and a few contact
-    # transitions; tools/fp32_floor.py --accel-noise shows the float64 oracle itself misses those steps under a
-    # 1e-4 relative per-substep acceleration perturbation
-    assert frac >= 0.94
-    assert np.median(e) <= 3e-5
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    # fp32 physics over a float64 master state in a z-shifted frame, contact geometry (narrowphase) and the Newton
+    # iterate in float64: measured 98.96 % (96 steps: one miss, the first landing impact at step 6,
+    # 1.7e-3) and 99.33 % (300 steps: the landing and step 166, where a cube spinning at 8.8 rad/s is struck -- a
+    # chaotic contact event, 0.13).  The landing miss is the impact's angular velocity (1e-4 rad/s): a small
+    # difference of large corner forces solved with the fp32 Hessian
+    if which == "short":
+        assert frac >= 0.985 and e.max() <= 2.5e-3, (frac, e.max())
+    else:
+        assert frac >= 0.99 and np.sort(e)[-2] <= 1e-3 and e.max() <= 0.2, (frac, np.sort(e)[-3:])
+    assert np.median(e) <= 1e-5
     # the same algorithm in plain single precision (liboracle_f32.so, tools/fp32_floor.py --float-oracle) on the
     # same trajectory: the kernel (float64 master state, z-shifted frame) must hold the gate at least as often,
     # and on the 96-step trajectory every step the kernel misses is one the float restatement misses too
@@ -226,17 +229,16 @@ def test_teacher_forced_long_fp64(oracle, A_, K_, T, seed):
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 def test_fp32_other_scenes_within_survey_gate(oracle):
     """fp32 (2, 8) and (2, 10) compile-time scenes over long trajectories: integer state / flags exact, the
-    SURVEY gate on >= 94 % of env-steps (measured 95.0 % and 95.2 %)"""
-    for A_, K_, T, seed in [(2, 8, 300, 5), (2, 10, 250, 9)]:
+    SURVEY gate on >= 98.5 % / 98 % of env-steps (measured 98.66 % and 98.39 %) with the worst step capped (measured
+    3.1e-3 and 1.1e-3)"""
+    for A_, K_, T, seed, gate, cap in [(2, 8, 300, 5, 0.985, 5e-3), (2, 10, 250, 9, 0.98, 2e-3)]:
         traj = _rollout(oracle, A_, K_, T, seed_actions=seed)
         r = _compare(traj, "fp32", 1e-4, A_, K_)
         frac = float(np.mean(r["errs"] <= 1e-4))
-        print(f"fp32 ({A_},{K_}): {frac:.1%} of {len(r['errs'])} steps within 1e-4; median {np.median(r['errs']):.2e}")
-        # integer task state: a cube whose fp32 position lands on the other side of a TaskManager bound
-        # (bucket / out-of-reach) flips a discrete decision -- the SURVEY expects such rare edge cases and asks
-        # for their rate (tools/flag_divergence.py); here at most 1 % of the steps
-        assert len(r["flag_bad"]) + len(r["int_bad"]) <= 0.01 * len(r["errs"]), (r["flag_bad"], r["int_bad"])
-        assert frac >= 0.94
+        print(f"fp32 ({A_},{K_}): {frac:.1%} of {len(r['errs'])} steps within 1e-4; median {np.median(r['errs']):.2e}, "
+              f"worst {r['errs'].max():.2e}")
+        assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+        assert frac >= gate and r["errs"].max() <= cap, (frac, r["errs"].max())
         assert frac >= _float_floor(A_, K_, T, seed)["within"]  # plain-float restatement: 53.5 % / 75.9 %
 
 
@@ -271,7 +273,7 @@ def test_masked_reset_only_touches_masked_arenas():
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 def test_config5_scene_4x16_pause_toggle_fp32(oracle):
-    """BASELINE config 5's arena (4 arms x 16 cubes, PauseIKToggleEnv, runtime-dims kernel, contact capacity
+    """BASELINE config 5's arena (4 arms x 16 cubes, PauseIKToggleEnv, compile-time fp32 kernel, contact capacity
     128 -- the 16 parked cubes alone hold 64 floor contacts): teacher-forced against the oracle over 60 env-steps
     from reset; no contact dropped for capacity, IK / task integer state exact, the SURVEY gate on most steps"""
     traj = pu.rollout(oracle, 4, 16, 60, seed_actions=17, env_class="PauseIKToggleEnv")
@@ -283,11 +285,12 @@ def test_config5_scene_4x16_pause_toggle_fp32(oracle):
           f"dropped {int(r['counters'][:, 0].sum())}")
     assert r["counters"][:, 0].sum() == 0
     assert r["counters"][:, 5].max() > 64  # the scene does exceed the benchmark scene's 64
-    assert len(r["flag_bad"]) + len(r["int_bad"]) <= 1
-    # measured 71 % (median 9.7e-6): at K = 16 most cubes sit parked on the floor at x = 4..5 m, where float
-    # spacing (4.8e-7 m) in the contact points of their resting contacts shows up as spin noise of those
-    # (task-irrelevant) cubes; the fp64 build is the parity build for this scene shape
-    assert frac >= 0.65
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    # compile-time (4,16) fp32 kernel; measured 91.2 % over 150 env-steps of another seed (round 2: 71 % with the
+    # float narrowphase).  At K = 16 most cubes sit parked on the floor at x = 4..5 m, where the float contact
+    # points of their resting contacts show up as spin noise of those (task-irrelevant) cubes; the fp64 build is
+    # the parity build for this scene shape
+    assert frac >= 0.85
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
