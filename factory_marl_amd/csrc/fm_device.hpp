@@ -2245,9 +2245,6 @@ __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_
 //  * Tree-block sparsity: H couples two trees only through a contact between them.  The coupling graph (plus
 //    the fill-in of this elimination order) comes from the tree->contact masks; a pivot updates only the row
 //    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
-#ifndef FM_CHOL_REFINE
-#define FM_CHOL_REFINE 1  // fp32 register Cholesky: one float64-residual refinement of the Newton direction
-#endif
 template <typename T, typename DIM>
 __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
                                                T* dir) {
@@ -2328,45 +2325,23 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
       });
     }
   });
-  // L L' x = rhs with the factor in registers (forward, then backward substitution)
-  auto solve = [&](T rhs) -> T {
-    T acc = rhs;
-    T y = T(0);
+  T acc = j < NV ? (T)-g[jo] : T(0);
+  T y = T(0);
 #pragma unroll
-    for (int k = 0; k < NV; k++) {
-      const T yk = readlane(acc * dinv, k);
-      if (j == k) y = yk;
-      if (j > k) acc -= col[k] * yk;
-    }
-    T acc2 = y, x = T(0);
+  for (int k = 0; k < NV; k++) {
+    const T yk = readlane(acc * dinv, k);
+    if (j == k) y = yk;
+    if (j > k) acc -= col[k] * yk;
+  }
+  T acc2 = y, x = T(0);
 #pragma unroll
-    for (int k = NV - 1; k >= 0; k--) {
-      const T xk = readlane(acc2 * dinv, k);
-      if (j == k) x = xk;
-      if (j < k) acc2 -= col[k] * dinv * xk;
-    }
-    return x;
-  };
-  T x = solve(j < NV ? (T)-g[jo] : T(0));
+  for (int k = NV - 1; k >= 0; k--) {
+    const T xk = readlane(acc2 * dinv, k);
+    if (j == k) x = xk;
+    if (j < k) acc2 -= col[k] * dinv * xk;
+  }
   if (j < NV) dir[jo] = x;
   SYNC();
-  if constexpr (sizeof(T) == 4 && FM_CHOL_REFINE) {
-    // one step of iterative refinement: the residual of H x = -g in float64 (H is intact in LDS: the factor lives
-    // in registers), solved with the same factor.  The fp32 factor's error (~ nv eps cond(H)) otherwise stays in
-    // the Newton direction, and with MuJoCo's tolerance Newton stops after that one direction
-    double r = j < NV ? -g[jo] : 0.0;
-    if (j < NV) {
-#pragma unroll
-      for (int i = 0; i < NV; i++) {
-        const int io = i == NV - 1 ? 0 : i + 1;
-        r -= (double)H[jo * NV + io] * (double)dir[io];
-      }
-    }
-    SYNC();
-    x += solve((T)r);
-    if (j < NV) dir[jo] = x;
-    SYNC();
-  }
 }
 
 // fp32, compile-time scene with 64 < nv <= 80 ((2,8), (2,10)): the same register Cholesky for the 64 leading
