@@ -60,6 +60,7 @@ constexpr int MAXPC = 8;      // contacts per geom pair (box-box)
 struct Dims {
   static constexpr bool fixed = false;  // runtime dims (see FixedDims for compile-time scenes)
   static constexpr bool spill = false;  // Hessian + contact records in LDS (see DimsSpill)
+  static constexpr bool midcache = false;  // cached midphase (FixedDims of the large scenes)
   static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
@@ -221,6 +222,7 @@ struct Lay {
   int scal;   // double [4]   per-step scalars broadcast from lane 0
   int prof;   // uint64 [FM_NPROF]  phase clocks of this arena (profiling only)
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
+  int mcache, mpos;  // cached midphase: uint32 [MC_CAP] hit list, T [ncb][4] body positions at the build
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -267,7 +269,12 @@ enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_
        PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_KHZ, PH_CBOUND, PH_CMID, PH_CNARROW, PH_CHDIAG, PH_CHPANEL, PH_CHTRAIL,
        PH_CHSOLVE, PH_LAST = 23, FM_NPROF = 24 };
 enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE, MISC_CSUM,
-       MISC_CMAX };
+       MISC_CMAX, MISC_MC_OK, MISC_MC_N, MISC_MC_TOT };
+// cached midphase (scenes with DIM::midcache): the body-pair hit list of an inflated bounding test is reused across
+// substeps until a moving collision body has travelled MC_HALF from where it was when the list was built
+constexpr int MC_CAP = 256;         // hit pairs a cached list holds (more: no caching that substep)
+constexpr double MC_MARGIN = 0.04;  // m added to every bound (sphere radius, plane distance)
+constexpr double MC_HALF = 0.02;    // rebuild once any moving body has moved this far (both ends: MC_MARGIN)
 // per-arena int64 counters (fm_get_counters): contacts dropped for capacity, Newton iterations, Newton
 // max-iteration hits, bucket-index anomalies, contacts summed over stages, max contacts in one stage,
 // objects in scene summed over env-steps, episodes ended
@@ -453,7 +460,8 @@ __host__ __device__ constexpr int hstride(int tsize, int nv) { return (tsize == 
 __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4 && nv > 80) ? 256 : 0; }
 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
-                                              int maxrow, int ntree, int tsize, bool spill = false) {
+                                              int maxrow, int ntree, int tsize, bool spill = false,
+                                              bool midcache = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -522,6 +530,10 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.uctl = take(8 * nu);
   L.scal = take(8 * 4);
   L.prof = take(8 * FM_NPROF);
+  if (midcache) {
+    L.mcache = take(4 * MC_CAP);
+    L.mpos = take(tsize * 4 * ncb);
+  }
   L.total = off;
   if (spill) {  // the two largest arrays in the arena's global scratch block (L2 / HBM) instead of LDS
     L.spill = 1;
@@ -549,6 +561,7 @@ struct FixedDims {
   static constexpr bool fixed = true;
   static constexpr bool spill = false;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
+  static constexpr bool midcache = nv > 80;  // (4,16): 65 collision bodies, 2080 pairs, LDS room to spare
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;
   static constexpr int MAXC = (A_ == 2 && K_ == 4) ? MAXCON : MAXCON_WIDE;
@@ -560,7 +573,7 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS);
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, false, midcache);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -288,6 +288,22 @@ struct Ws {
       return (T*)(base + L->Marm);
     }
   }
+  __device__ __forceinline__ uint32_t* mcache() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (uint32_t*)(base + c.mcache);
+    } else {
+      return (uint32_t*)(base + L->mcache);
+    }
+  }
+  __device__ __forceinline__ T* mpos() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (T*)(base + c.mpos);
+    } else {
+      return (T*)(base + L->mpos);
+    }
+  }
   __device__ __forceinline__ T* gx() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -1248,9 +1264,33 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   SYNC();
   PMARK(PH_CBOUND);
   // 3. midphase: every allowed body pair's bounding test; the hits are compacted into sp[] (body pair | first
-  // geom-pair index << 16) in one sweep, so the geom-pair expansion below runs over all of them at once
+  // geom-pair index << 16) in one sweep, so the geom-pair expansion below runs over all of them at once.
+  // DIM::midcache: the list of an inflated test (every bound + MC_MARGIN) is kept and reused while no moving
+  // body has moved MC_HALF since it was built -- a pair outside the inflated test then cannot pass the exact one,
+  // and the geom-pair test and narrowphase below decide the contacts as before (so the contact set is unchanged)
   uint32_t* sp = w.sp();
   int nsp = 0, total = 0;
+  bool reuse = false;
+  T infl = T(0);
+  if constexpr (DIM::midcache) {
+    bool moved = false;
+    const int ok = misc[MISC_MC_OK];
+    for (int b = LANE; b < dm.ncb; b += WAVE) {
+      const T* o = w.cbw() + 8 * b;
+      const T* p0 = w.mpos() + 4 * b;
+      const T dx = fabs(o[0] - p0[0]), dy = fabs(o[1] - p0[1]), dz = fabs(o[2] - p0[2]);
+      const T dmax = dx > dy ? (dx > dz ? dx : dz) : (dy > dz ? dy : dz);
+      moved = moved || !(dmax <= T(MC_HALF));
+    }
+    reuse = ok && __ballot(moved) == 0ull;
+    if (reuse) {
+      sp = w.mcache();
+      nsp = misc[MISC_MC_N];
+      total = misc[MISC_MC_TOT];
+    } else {
+      infl = T(MC_MARGIN);
+    }
+  }
   auto sweep = [&](uint32_t bpw, int pidx) {
     // branch-free: both records and both flag words are read unconditionally (a lane past the list reads body
     // 0's), so each pass is one batch of LDS reads
@@ -1264,9 +1304,9 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     d0 = d0 > T(0) ? d0 : T(0);
     d1 = d1 > T(0) ? d1 : T(0);
     d2 = d2 > T(0) ? d2 : T(0);
-    const T rr = X[3] + Y[3];
+    const T rr = X[3] + Y[3] + infl;
     const bool hs = d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr;
-    const T zf = T(-zshift<T>());  // the floor's height in the kernel frame
+    const T zf = T(-zshift<T>()) + infl;  // the floor's height in the kernel frame (+ the cache margin)
     const bool hp1 = Y[2] - Y[6] - Y[3] <= zf, hp2 = X[2] - X[6] - X[3] <= zf;
     const bool hit = pidx < dm.ncbp && ((f1 & CB_PLANE) ? hp1 : ((f2 & CB_PLANE) ? hp2 : hs));
     const int ncomb = hit ? n1 * n2 : 0;
@@ -1277,9 +1317,28 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     total += __builtin_amdgcn_readlane(incl, WAVE - 1);
   };
   if constexpr (DIM::fixed) {
+    if (!reuse) {
 #pragma unroll
-    for (int k = 0; k < NPP; k++)
-      if (k * WAVE < dm.ncbp) sweep(bpr[k], k * WAVE + LANE);
+      for (int k = 0; k < NPP; k++)
+        if (k * WAVE < dm.ncbp) sweep(bpr[k], k * WAVE + LANE);
+      if constexpr (DIM::midcache) {
+        // keep the inflated list (when it fits) and the positions it was built at
+        const bool fits = nsp <= MC_CAP;
+        for (int e = LANE; e < nsp && fits; e += WAVE) w.mcache()[e] = sp[e];
+        for (int b = LANE; b < dm.ncb; b += WAVE) {
+          const T* o = w.cbw() + 8 * b;
+          T* p0 = w.mpos() + 4 * b;
+          p0[0] = o[0];
+          p0[1] = o[1];
+          p0[2] = o[2];
+        }
+        if (LANE == 0) {
+          misc[MISC_MC_OK] = fits ? 1 : 0;
+          misc[MISC_MC_N] = nsp;
+          misc[MISC_MC_TOT] = total;
+        }
+      }
+    }
   } else {
     // allowed body pairs are fetched one pass ahead (the global load overlaps the current pass)
     uint32_t bpw_next = LANE < dm.ncbp ? M.cbp[LANE] : 0u;
@@ -4079,6 +4138,7 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   if (LANE == 0) {
     w.misc()[MISC_CSUM] = 0;
     w.misc()[MISC_CMAX] = 0;
+    w.misc()[MISC_MC_OK] = 0;  // the cached midphase list is rebuilt at the first substep of every launch
   }
 #define ti (S.ints + (size_t)arena * dm.int_stride)
 #define td (S.dbl + (size_t)arena * dm.dbl_stride + nu)  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
