@@ -561,7 +561,7 @@ struct FixedDims {
   static constexpr bool fixed = true;
   static constexpr bool spill = false;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
-  static constexpr bool midcache = nv > 80;  // (4,16): 65 collision bodies, 2080 pairs, LDS room to spare
+  static constexpr bool midcache = nv > 48;  // (2,8), (2,10), (4,16): LDS room within their occupancy (not (2,4))
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;
   static constexpr int MAXC = (A_ == 2 && K_ == 4) ? MAXCON : MAXCON_WIDE;
