@@ -121,7 +121,8 @@ def timed_run(ctx, args, precision, steps, warmup, lo, hi):
     A, K, N = args.arms, args.objects, hi - lo
     env = FactoryVecEnv(N, env_class=args.env_class,
                         env_kwargs=run_kwargs(args.env_class, num_arms=A, max_num_objects=K, seed=42),
-                        device=ctx.local_rank, precision=precision, seeds=arena_seeds(lo, hi, args.seeds))
+                        device=ctx.local_rank, precision=precision, seeds=arena_seeds(lo, hi, args.seeds),
+                        solver_tolerance=args.solver_tolerance)
     env.reset()
     preroll(env, args.preroll, ctx.rank, ctx.device)
     g = torch.Generator(device=ctx.device)
@@ -163,7 +164,8 @@ def timed_run_ppo(ctx, args, lo, hi):
     A, K, N = args.arms, args.objects, hi - lo
     env = FactoryVecEnv(N, env_kwargs=run_kwargs(args.env_class, num_arms=A, max_num_objects=K, seed=42),
                         device=ctx.local_rank,
-                        precision=args.precision, seeds=arena_seeds(lo, hi, args.seeds))
+                        precision=args.precision, seeds=arena_seeds(lo, hi, args.seeds),
+                        solver_tolerance=args.solver_tolerance)
     env.reset()
     preroll(env, args.preroll, ctx.rank, ctx.device)
     dist = None
@@ -310,6 +312,8 @@ def main():
     ap.add_argument("--seeds", default="fixed", choices=["fixed", "arena"],
                     help="scene/TaskManager seed: 42 everywhere (saved runs) or 42 + global arena id")
     ap.add_argument("--fp64-steps", type=int, default=30, help="also time the fp64 build (0 = skip)")
+    ap.add_argument("--solver-tolerance", type=float, default=0.0,
+                    help="Newton tolerance (0 = the precision's default, fm_create)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
