@@ -634,7 +634,8 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
     delete h;
     return set_err(FM_EINVAL, "num_arms > 16");
   }
-  if (h->cfg.solver_tolerance <= 0) h->cfg.solver_tolerance = h->fp64 ? 1e-12 : 1e-7;
+  // fp32: MuJoCo's own default (opt.tolerance 1e-8, the reference's setting); fp64: the oracle's 1e-12
+  if (h->cfg.solver_tolerance <= 0) h->cfg.solver_tolerance = h->fp64 ? 1e-12 : 1e-8;
   if (h->cfg.solver_iterations <= 0) h->cfg.solver_iterations = 100;
   std::string err;
   if (!build_scene(cfg->num_arms, cfg->max_num_objects, cfg->num_arenas, seeds, h->sc, err)) {

@@ -273,8 +273,11 @@ enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, M
 // cached midphase (scenes with DIM::midcache): the body-pair hit list of an inflated bounding test is reused across
 // substeps until a moving collision body has travelled MC_HALF from where it was when the list was built
 constexpr int MC_CAP = 256;         // hit pairs a cached list holds (more: no caching that substep)
-constexpr double MC_MARGIN = 0.04;  // m added to every bound (sphere radius, plane distance)
-constexpr double MC_HALF = 0.02;    // rebuild once any moving body has moved this far (both ends: MC_MARGIN)
+#ifndef FM_MC_MARGIN
+#define FM_MC_MARGIN 0.04
+#endif
+constexpr double MC_MARGIN = FM_MC_MARGIN;    // m added to every bound (sphere radius, plane distance)
+constexpr double MC_HALF = 0.5 * MC_MARGIN;  // rebuild once any moving body has moved this far (both ends: MC_MARGIN)
 // per-arena int64 counters (fm_get_counters): contacts dropped for capacity, Newton iterations, Newton
 // max-iteration hits, bucket-index anomalies, contacts summed over stages, max contacts in one stage,
 // objects in scene summed over env-steps, episodes ended

@@ -89,12 +89,11 @@ def test_teacher_forced_fp32(trajectory, long_trajectory, which):
           f"missing steps {list(r['err_steps'][e > 1e-4])}")
     assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
     # fp32 physics over a float64 master state in a z-shifted frame, contact geometry (narrowphase) and the Newton
-    # iterate in float64: measured 98.96 % (96 steps: one miss, the first landing impact at step 6,
-    # 1.7e-3) and 99.33 % (300 steps: the landing and step 166, where a cube spinning at 8.8 rad/s is struck -- a
-    # chaotic contact event, 0.13).  The landing miss is the impact's angular velocity (1e-4 rad/s): a small
-    # difference of large corner forces solved with the fp32 Hessian
+    # iterate in float64, MuJoCo's 1e-8 Newton tolerance: measured 98.96 % (96 steps: one miss, the
+    # first landing impact at step 6, 2.3e-4) and 99.33 % (300 steps: the landing and step 166, where a cube spinning
+    # at 8.8 rad/s is struck -- a chaotic contact event, 0.13; the fp64 build matches it to 1e-10)
     if which == "short":
-        assert frac >= 0.985 and e.max() <= 2.5e-3, (frac, e.max())
+        assert frac >= 0.985 and e.max() <= 5e-4, (frac, e.max())
     else:
         assert frac >= 0.99 and np.sort(e)[-2] <= 1e-3 and e.max() <= 0.2, (frac, np.sort(e)[-3:])
     assert np.median(e) <= 1e-5
@@ -229,9 +228,9 @@ def test_teacher_forced_long_fp64(oracle, A_, K_, T, seed):
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 def test_fp32_other_scenes_within_survey_gate(oracle):
     """fp32 (2, 8) and (2, 10) compile-time scenes over long trajectories: integer state / flags exact, the
-    SURVEY gate on >= 98.5 % / 98 % of env-steps (measured 98.66 % and 98.39 %) with the worst step capped (measured
-    3.1e-3 and 1.1e-3)"""
-    for A_, K_, T, seed, gate, cap in [(2, 8, 300, 5, 0.985, 5e-3), (2, 10, 250, 9, 0.98, 2e-3)]:
+    SURVEY gate on >= 99 % of env-steps (measured 99.0 % and 99.2 %) with the worst step capped (measured 3.1e-3 and
+    1.1e-3; a 1e-9 Newton tolerance brings both under 1.7e-4)"""
+    for A_, K_, T, seed, gate, cap in [(2, 8, 300, 5, 0.99, 5e-3), (2, 10, 250, 9, 0.99, 2e-3)]:
         traj = _rollout(oracle, A_, K_, T, seed_actions=seed)
         r = _compare(traj, "fp32", 1e-4, A_, K_)
         frac = float(np.mean(r["errs"] <= 1e-4))
