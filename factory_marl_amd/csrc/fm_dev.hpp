@@ -274,7 +274,7 @@ enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, M
 // substeps until a moving collision body has travelled MC_HALF from where it was when the list was built
 constexpr int MC_CAP = 256;         // hit pairs a cached list holds (more: no caching that substep)
 #ifndef FM_MC_MARGIN
-#define FM_MC_MARGIN 0.04
+#define FM_MC_MARGIN 0.01  // measured 4 / 2 / 1 cm: (4,16) equal, (2,8) best at 1 cm (gpurun_out/r03n)
 #endif
 constexpr double MC_MARGIN = FM_MC_MARGIN;    // m added to every bound (sphere radius, plane distance)
 constexpr double MC_HALF = 0.5 * MC_MARGIN;  // rebuild once any moving body has moved this far (both ends: MC_MARGIN)

@@ -2722,6 +2722,7 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
   const int j = LANE, j16 = j & 15, q4 = j >> 4;
   float* dinv = (float*)w.tmp();  // [hs] 1 / L_kk (quad()'s scratch, dead until the line search)
   float* IL = H + hs * hs;        // [16][16] L_bb^-1 of the current block (hextra)
+  uint64_t* nzs = (uint64_t*)w.bc();  // [nb] nonzero panel tiles of each block (bc: unused above 64 dofs)
   const float tiny = 1e-37f;
   for (int b = 0; b < nb; b++) {
     const int c0 = 16 * b;
@@ -2770,7 +2771,10 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
     }
     SYNC();
     PMARK(PH_CHDIAG);
-    // ---- panel: P = H_panel L_bb^-T, tile rows below the block
+    // ---- panel: P = H_panel L_bb^-T, tile rows below the block.  H is block-sparse (trees couple only through
+    // contacts; most cubes of a (4,16) arena rest alone): a tile whose H_panel is all zero has P = 0 and
+    // contributes nothing below, so it is skipped here and in the trailing update (bit t of nz: tile row t)
+    uint64_t nz = 0;
     {
       float bo[4];
 #pragma unroll
@@ -2779,6 +2783,8 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
         float a[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) a[s] = H[(rI + j16) * hs + c0 + 4 * s + q4];
+        if (__ballot(a[0] != 0.0f || a[1] != 0.0f || a[2] != 0.0f || a[3] != 0.0f) == 0ull) continue;
+        nz |= 1ull << (rI >> 4);
         fm_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[s], acc, 0, 0, 0);
@@ -2787,24 +2793,35 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
         for (int r = 0; r < 4; r++) H[(rI + 4 * q4 + r) * hs + c0 + j16] = acc[r];
       }
     }
+    if (LANE == 0) nzs[b] = nz;
     SYNC();
     PMARK(PH_CHPANEL);
-    // ---- trailing update of the lower-triangle tiles (I >= J) after the block, two tiles per pass
-    {
-      const int t0 = b + 1;
-      const int nt = nb - t0;
-      const int ntile = nt * (nt + 1) / 2;
-      int I = 0, J = 0;  // tile t -> (I, J), walked incrementally
-      for (int t = 0; t < ntile; t += 2) {
-        const int I1 = I, J1 = J;
-        int I2 = I1, J2 = J1 + 1;
-        if (J2 > I2) {
-          I2++;
-          J2 = 0;
+    // ---- trailing update of the lower-triangle tiles (I >= J) whose panel tiles are both nonzero, two tiles
+    // per pass (pairs walked over the set bits of nz: I ascending, J <= I)
+    if (nz) {
+      int I = __builtin_ctzll(nz), J = I;
+      bool more = true;
+      auto advance = [&]() {
+        const uint64_t after = J < 63 ? nz & (~0ull << (J + 1)) : 0ull;
+        if (after && __builtin_ctzll(after) <= I) {
+          J = __builtin_ctzll(after);
+        } else {
+          const uint64_t nextI = I < 63 ? nz & (~0ull << (I + 1)) : 0ull;
+          if (!nextI) {
+            more = false;
+          } else {
+            I = __builtin_ctzll(nextI);
+            J = __builtin_ctzll(nz);
+          }
         }
-        const bool two = t + 1 < ntile;
-        const int rI1 = 16 * (t0 + I1), rJ1 = 16 * (t0 + J1);
-        const int rI2 = 16 * (t0 + (two ? I2 : I1)), rJ2 = 16 * (t0 + (two ? J2 : J1));
+      };
+      while (more) {
+        const int I1 = I, J1 = J;
+        advance();
+        const bool two = more;
+        const int I2 = two ? I : I1, J2 = two ? J : J1;
+        if (two) advance();
+        const int rI1 = 16 * I1, rJ1 = 16 * J1, rI2 = 16 * I2, rJ2 = 16 * J2;
         float a1[4], b1[4], a2[4], b2[4];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
@@ -2831,12 +2848,6 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
         if (two) {
 #pragma unroll
           for (int r = 0; r < 4; r++) H[(rI2 + 4 * q4 + r) * hs + rJ2 + j16] = c2[r] - acc2[r];
-        }
-        I = I2;
-        J = J2 + 1;
-        if (J > I) {
-          I++;
-          J = 0;
         }
       }
     }
@@ -2866,7 +2877,9 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
     for (int k = 0; k < 16; k++) yb[k] = readlane(y, k);
     SYNC();
     if (own) dir[c0 + j] = y;
+    const uint64_t nzb = nzs[b];
     for (int r = c0 + 16 + j; r < nv; r += WAVE) {
+      if (!((nzb >> (r >> 4)) & 1ull)) continue;  // a zero panel tile: nothing to subtract
       float lr[16];
 #pragma unroll
       for (int k = 0; k < 16; k++) lr[k] = H[r * hs + c0 + k];
@@ -2899,6 +2912,7 @@ __device__ __forceinline__ void chol_dense_mfma(const Model<float>& M, const Ws<
     SYNC();
     if (own) dir[c0 + j] = x;
     for (int r = j; r < c0; r += WAVE) {
+      if (!((nzs[r >> 4] >> b) & 1ull)) continue;  // L[c0 .. c0 + 15][r] lies in a zero panel tile of block r / 16
       float lc[16];
 #pragma unroll
       for (int k = 0; k < 16; k++) lc[k] = H[(c0 + k) * hs + r];
