@@ -222,7 +222,7 @@ struct Lay {
   int scal;   // double [4]   per-step scalars broadcast from lane 0
   int prof;   // uint64 [FM_NPROF]  phase clocks of this arena (profiling only)
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
-  int mcache, mpos;  // cached midphase: uint32 [MC_CAP] hit list, T [ncb][4] body positions at the build
+  int mcache, mpos;  // cached midphase: uint32 [mc_cap(nv)] hit list, T [ncb][3] body positions at the build
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -272,7 +272,9 @@ enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, M
        MISC_CMAX, MISC_MC_OK, MISC_MC_N, MISC_MC_TOT };
 // cached midphase (scenes with DIM::midcache): the body-pair hit list of an inflated bounding test is reused across
 // substeps until a moving collision body has travelled MC_HALF from where it was when the list was built
-constexpr int MC_CAP = 256;         // hit pairs a cached list holds (more: no caching that substep)
+// hit pairs a cached list holds (more: no caching that substep); the (2,4) scene has LDS room for 40 within its
+// 4-arenas-per-CU budget
+__host__ __device__ constexpr int mc_cap(int nv) { return nv > 48 ? 256 : 40; }
 #ifndef FM_MC_MARGIN
 #define FM_MC_MARGIN 0.01  // measured 4 / 2 / 1 cm: (4,16) equal, (2,8) best at 1 cm (gpurun_out/r03n)
 #endif
@@ -464,7 +466,7 @@ __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4
 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
-                                              bool midcache = false) {
+                                              bool midcache = false, bool nobc = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -473,7 +475,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
     return o;
   };
   // lane-broadcast row first: within ds_read2's 1 KiB offset reach of the workspace base
-  L.bc = take(tsize * WAVE);
+  L.bc = take(nobc ? 0 : tsize * WAVE);  // unused by the (2,4) kernel's register Cholesky
   L.q = take(tsize * nq);
   L.v = take(tsize * nv);
   L.a = take(8 * nv);  // Newton iterate (float64 in both builds; the next substep's warmstart)
@@ -534,8 +536,8 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.scal = take(8 * 4);
   L.prof = take(8 * FM_NPROF);
   if (midcache) {
-    L.mcache = take(4 * MC_CAP);
-    L.mpos = take(tsize * 4 * ncb);
+    L.mcache = take(4 * mc_cap(nv));
+    L.mpos = take(tsize * 3 * ncb);
   }
   L.total = off;
   if (spill) {  // the two largest arrays in the arena's global scratch block (L2 / HBM) instead of LDS
@@ -564,7 +566,7 @@ struct FixedDims {
   static constexpr bool fixed = true;
   static constexpr bool spill = false;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
-  static constexpr bool midcache = nv > 48;  // (2,8), (2,10), (4,16): LDS room within their occupancy (not (2,4))
+  static constexpr bool midcache = true;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;
   static constexpr int MAXC = (A_ == 2 && K_ == 4) ? MAXCON : MAXCON_WIDE;
@@ -576,7 +578,7 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, false, midcache);
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, false, midcache, MAXC == WAVE);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -1277,7 +1277,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     const int ok = misc[MISC_MC_OK];
     for (int b = LANE; b < dm.ncb; b += WAVE) {
       const T* o = w.cbw() + 8 * b;
-      const T* p0 = w.mpos() + 4 * b;
+      const T* p0 = w.mpos() + 3 * b;
       const T dx = fabs(o[0] - p0[0]), dy = fabs(o[1] - p0[1]), dz = fabs(o[2] - p0[2]);
       const T dmax = dx > dy ? (dx > dz ? dx : dz) : (dy > dz ? dy : dz);
       moved = moved || !(dmax <= T(MC_HALF));
@@ -1323,11 +1323,11 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
         if (k * WAVE < dm.ncbp) sweep(bpr[k], k * WAVE + LANE);
       if constexpr (DIM::midcache) {
         // keep the inflated list (when it fits) and the positions it was built at
-        const bool fits = nsp <= MC_CAP;
+        const bool fits = nsp <= mc_cap(DIM::nv);
         for (int e = LANE; e < nsp && fits; e += WAVE) w.mcache()[e] = sp[e];
         for (int b = LANE; b < dm.ncb; b += WAVE) {
           const T* o = w.cbw() + 8 * b;
-          T* p0 = w.mpos() + 4 * b;
+          T* p0 = w.mpos() + 3 * b;
           p0[0] = o[0];
           p0[1] = o[1];
           p0[2] = o[2];

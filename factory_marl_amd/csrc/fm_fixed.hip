@@ -16,6 +16,11 @@
 
 namespace fm {
 
+// the benchmark scene keeps 4 arenas (one wave per SIMD) per CU: its fp32 workspace must stay within a quarter of
+// the CU's 160 KiB of LDS (the midphase cache was sized to fit, fm_dev.hpp mc_cap)
+static_assert(!(FM_A == 2 && FM_K == 4 && FM_PREC == 32) || FixedDims<2, 4>::template layout<4>().total <= 160 * 1024 / 4,
+              "(2,4) fp32 workspace above 40 KiB: 3 arenas per CU");
+
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes) {
   hipError_t e = hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K>, false>,
