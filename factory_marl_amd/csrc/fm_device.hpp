@@ -763,6 +763,135 @@ struct BBSat {
   T face_s, edge_s, best_face, best_edge;
 };
 
+// face contact of a box pair: the reference box owns the best face axis, the incident box's face most
+// anti-parallel to it is clipped against the reference rectangle.  Setup (frames, the incident quad in reference
+// coordinates u, v, w) and the 24 candidate points in the serial order: (1) incident vertices inside the rectangle
+// (c 0-3), (2) reference corners inside the incident quad (c 4-7), (3) proper crossings of incident edge m with side sd
+// (c = 8 + 4 m + sd).  A candidate that exists and penetrates (w <= 0) is a contact.
+template <typename T>
+struct BBFace {
+  V3<T> n, nref, fc, ta, tb;
+  T e1, e2, cu, cv, cw, det, ia, ib;
+  T U[4], V[4], W[4];
+};
+template <typename T>
+__device__ __forceinline__ T pick4(int k, const T (&x)[4]) {
+  return k == 0 ? x[0] : (k == 1 ? x[1] : (k == 2 ? x[2] : x[3]));
+}
+template <typename T>
+__device__ __forceinline__ BBFace<T> bb_face_setup(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2,
+                                                   const T* h2, const BBSat<T>& sat) {
+  BBFace<T> F;
+  const V3<T> A[3] = {vcol(R1, 0), vcol(R1, 1), vcol(R1, 2)};
+  const V3<T> B[3] = {vcol(R2, 0), vcol(R2, 1), vcol(R2, 2)};
+  const V3<T> P1{p1[0], p1[1], p1[2]}, P2{p2[0], p2[1], p2[2]};
+  const int face_id = sat.face_id;
+  const V3<T> face_u = sat.face_u;
+  const T sg = sat.face_s >= T(0) ? T(1) : T(-1);
+  const V3<T> n{face_u.x * sg, face_u.y * sg, face_u.z * sg};
+  const bool ref1 = face_id < 3;
+  const int kr = ref1 ? face_id : face_id - 3;
+  const V3<T> Rr0 = vsel(ref1, A[0], B[0]), Rr1 = vsel(ref1, A[1], B[1]), Rr2 = vsel(ref1, A[2], B[2]);
+  const V3<T> Ri0 = vsel(ref1, B[0], A[0]), Ri1 = vsel(ref1, B[1], A[1]), Ri2 = vsel(ref1, B[2], A[2]);
+  const T hr0 = ref1 ? h1[0] : h2[0], hr1 = ref1 ? h1[1] : h2[1], hr2 = ref1 ? h1[2] : h2[2];
+  const T hi0 = ref1 ? h2[0] : h1[0], hi1 = ref1 ? h2[1] : h1[1], hi2 = ref1 ? h2[2] : h1[2];
+  const V3<T> pr = vsel(ref1, P1, P2), pi = vsel(ref1, P2, P1);
+  const V3<T> nref = ref1 ? n : V3<T>{-n.x, -n.y, -n.z};
+  const int t1 = (kr + 1) % 3, t2 = (kr + 2) % 3;
+  const T hrk = spick(kr, hr0, hr1, hr2);
+  const V3<T> fc{pr.x + nref.x * hrk, pr.y + nref.y * hrk, pr.z + nref.z * hrk};
+  const V3<T> ta = vpick(t1, Rr0, Rr1, Rr2), tb = vpick(t2, Rr0, Rr1, Rr2);
+  const T e1 = spick(t1, hr0, hr1, hr2), e2 = spick(t2, hr0, hr1, hr2);
+  // incident face: the incident box axis most anti-parallel to nref
+  const T dk0 = vdot(nref, Ri0), dk1 = vdot(nref, Ri1), dk2 = vdot(nref, Ri2);
+  int mi = 0;
+  T bestdot = fabs(dk0), dmi = dk0;
+  if (fabs(dk1) > bestdot) {
+    bestdot = fabs(dk1);
+    mi = 1;
+    dmi = dk1;
+  }
+  if (fabs(dk2) > bestdot) {
+    mi = 2;
+    dmi = dk2;
+  }
+  const T sgn = dmi > T(0) ? T(-1) : T(1);
+  const int u1 = (mi + 1) % 3, u2 = (mi + 2) % 3;
+  const T him = spick(mi, hi0, hi1, hi2), hu1 = spick(u1, hi0, hi1, hi2), hu2 = spick(u2, hi0, hi1, hi2);
+  const V3<T> am = vpick(mi, Ri0, Ri1, Ri2), a1 = vpick(u1, Ri0, Ri1, Ri2), a2 = vpick(u2, Ri0, Ri1, Ri2);
+  // incident face centre relative to the reference face centre, in reference coordinates (u, v, w)
+  const V3<T> icr{pi.x + sgn * him * am.x - fc.x, pi.y + sgn * him * am.y - fc.y, pi.z + sgn * him * am.z - fc.z};
+  const T cu = vdot(icr, ta), cv = vdot(icr, tb), cw = vdot(icr, nref);
+  const T a1u = hu1 * vdot(a1, ta), a1v = hu1 * vdot(a1, tb), a1w = hu1 * vdot(a1, nref);
+  const T a2u = hu2 * vdot(a2, ta), a2v = hu2 * vdot(a2, tb), a2w = hu2 * vdot(a2, nref);
+  const T sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    F.U[k] = cu + sx[k] * a1u + sy[k] * a2u;
+    F.V[k] = cv + sx[k] * a1v + sy[k] * a2v;
+    F.W[k] = cw + sx[k] * a1w + sy[k] * a2w;
+  }
+  F.n = n;
+  F.nref = nref;
+  F.fc = fc;
+  F.ta = ta;
+  F.tb = tb;
+  F.e1 = e1;
+  F.e2 = e2;
+  F.cu = cu;
+  F.cv = cv;
+  F.cw = cw;
+  F.det = a1u * a2v - a2u * a1v;
+  F.ia = a1w * a2v - a2w * a1v;
+  F.ib = a1u * a2w - a2u * a1w;
+  return F;
+}
+template <typename T>
+__device__ __forceinline__ bool bb_face_candidate(const BBFace<T>& F, int c, T& u, T& v, T& w) {
+  if (c < 4) {  // (1) incident vertex c
+    u = pick4(c, F.U);
+    v = pick4(c, F.V);
+    w = pick4(c, F.W);
+    return fabs(u) <= F.e1 && fabs(v) <= F.e2;
+  }
+  if (c < 8) {  // (2) reference corner c - 4, w on the incident plane
+    const int k = c - 4;
+    const T cu_ = (k == 0 || k == 3) ? F.e1 : -F.e1, cv_ = k < 2 ? F.e2 : -F.e2;
+    bool in = F.det != T(0);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int m1 = (m + 1) & 3;
+      T cr = (F.U[m1] - F.U[m]) * (cv_ - F.V[m]) - (F.V[m1] - F.V[m]) * (cu_ - F.U[m]);
+      in = in && (F.det >= T(0) ? cr > T(0) : cr < T(0));
+    }
+    u = cu_;
+    v = cv_;
+    w = F.cw + (F.ia * (cu_ - F.cu) + F.ib * (cv_ - F.cv)) / F.det;
+    return in;
+  }
+  // (3) incident edge m (vertex m -> m + 1) crossing rectangle side sd (u = +e1, -e1, v = +e2, -e2)
+  const int m = (c - 8) >> 2, sd = (c - 8) & 3, m1 = (m + 1) & 3;
+  const bool onu = sd < 2;
+  const T ss = (sd & 1) ? T(-1) : T(1);
+  const T e = onu ? F.e1 : F.e2;
+  const T Um = pick4(m, F.U), Um1 = pick4(m1, F.U), Vm = pick4(m, F.V), Vm1 = pick4(m1, F.V);
+  const T Wm = pick4(m, F.W), Wm1 = pick4(m1, F.W);
+  const T dp = e - ss * (onu ? Um : Vm);
+  const T dq = e - ss * (onu ? Um1 : Vm1);
+  if (!((dp > T(0) && dq < T(0)) || (dp < T(0) && dq > T(0)))) return false;
+  const T f = dp / (dp - dq);
+  u = Um + (Um1 - Um) * f;
+  v = Vm + (Vm1 - Vm) * f;
+  w = Wm + (Wm1 - Wm) * f;
+  return onu ? fabs(v) <= F.e2 : fabs(u) < F.e1;
+}
+template <typename T, typename E>
+__device__ __forceinline__ void bb_face_emit(const BBFace<T>& F, T u, T v, T w, E& emit) {
+  const T hw = T(0.5) * w;
+  emit(w, F.fc.x + u * F.ta.x + v * F.tb.x + hw * F.nref.x, F.fc.y + u * F.ta.y + v * F.tb.y + hw * F.nref.y,
+       F.fc.z + u * F.ta.z + v * F.tb.z + hw * F.nref.z, F.n.x, F.n.y, F.n.z);
+}
+
 template <typename T, typename E>
 __device__ __forceinline__ void np_box_box_finish(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2,
                                                   const T* h2, const BBSat<T>& sat, E& emit);
@@ -836,94 +965,12 @@ __device__ __forceinline__ void np_box_box_finish(const T* p1, const T* R1, cons
          T(0.5) * (e1.z + s * ai.z + e2.z + t * bj.z), n.x, n.y, n.z);
     return;
   }
-  // ---- face contact: reference box (owner of the face axis) and incident box
-  const T sg = face_s >= T(0) ? T(1) : T(-1);
-  const V3<T> n{face_u.x * sg, face_u.y * sg, face_u.z * sg};
-  const bool ref1 = face_id < 3;
-  const int kr = ref1 ? face_id : face_id - 3;
-  const V3<T> Rr0 = vsel(ref1, A[0], B[0]), Rr1 = vsel(ref1, A[1], B[1]), Rr2 = vsel(ref1, A[2], B[2]);
-  const V3<T> Ri0 = vsel(ref1, B[0], A[0]), Ri1 = vsel(ref1, B[1], A[1]), Ri2 = vsel(ref1, B[2], A[2]);
-  const T hr0 = ref1 ? h1[0] : h2[0], hr1 = ref1 ? h1[1] : h2[1], hr2 = ref1 ? h1[2] : h2[2];
-  const T hi0 = ref1 ? h2[0] : h1[0], hi1 = ref1 ? h2[1] : h1[1], hi2 = ref1 ? h2[2] : h1[2];
-  const V3<T> pr = vsel(ref1, P1, P2), pi = vsel(ref1, P2, P1);
-  const V3<T> nref = ref1 ? n : V3<T>{-n.x, -n.y, -n.z};
-  const int t1 = (kr + 1) % 3, t2 = (kr + 2) % 3;
-  const T hrk = spick(kr, hr0, hr1, hr2);
-  const V3<T> fc{pr.x + nref.x * hrk, pr.y + nref.y * hrk, pr.z + nref.z * hrk};
-  const V3<T> ta = vpick(t1, Rr0, Rr1, Rr2), tb = vpick(t2, Rr0, Rr1, Rr2);
-  const T e1 = spick(t1, hr0, hr1, hr2), e2 = spick(t2, hr0, hr1, hr2);
-  // incident face: the incident box axis most anti-parallel to nref
-  const T dk0 = vdot(nref, Ri0), dk1 = vdot(nref, Ri1), dk2 = vdot(nref, Ri2);
-  int mi = 0;
-  T bestdot = fabs(dk0), dmi = dk0;
-  if (fabs(dk1) > bestdot) {
-    bestdot = fabs(dk1);
-    mi = 1;
-    dmi = dk1;
-  }
-  if (fabs(dk2) > bestdot) {
-    mi = 2;
-    dmi = dk2;
-  }
-  const T sgn = dmi > T(0) ? T(-1) : T(1);
-  const int u1 = (mi + 1) % 3, u2 = (mi + 2) % 3;
-  const T him = spick(mi, hi0, hi1, hi2), hu1 = spick(u1, hi0, hi1, hi2), hu2 = spick(u2, hi0, hi1, hi2);
-  const V3<T> am = vpick(mi, Ri0, Ri1, Ri2), a1 = vpick(u1, Ri0, Ri1, Ri2), a2 = vpick(u2, Ri0, Ri1, Ri2);
-  // incident face centre relative to the reference face centre, in reference coordinates (u, v, w)
-  const V3<T> icr{pi.x + sgn * him * am.x - fc.x, pi.y + sgn * him * am.y - fc.y, pi.z + sgn * him * am.z - fc.z};
-  const T cu = vdot(icr, ta), cv = vdot(icr, tb), cw = vdot(icr, nref);
-  const T a1u = hu1 * vdot(a1, ta), a1v = hu1 * vdot(a1, tb), a1w = hu1 * vdot(a1, nref);
-  const T a2u = hu2 * vdot(a2, ta), a2v = hu2 * vdot(a2, tb), a2w = hu2 * vdot(a2, nref);
-  const T sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
-  T U[4], V[4], W[4];
+  // ---- face contact: the candidates in the serial order (incident vertices, reference corners, crossings)
+  const BBFace<T> F = bb_face_setup(p1, R1, h1, p2, R2, h2, sat);
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    U[k] = cu + sx[k] * a1u + sy[k] * a2u;
-    V[k] = cv + sx[k] * a1v + sy[k] * a2v;
-    W[k] = cw + sx[k] * a1w + sy[k] * a2w;
-  }
-  auto out = [&](T u, T v, T w) {
-    if (w > T(0)) return;  // not penetrating
-    T hw = T(0.5) * w;
-    emit(w, fc.x + u * ta.x + v * tb.x + hw * nref.x, fc.y + u * ta.y + v * tb.y + hw * nref.y,
-         fc.z + u * ta.z + v * tb.z + hw * nref.z, n.x, n.y, n.z);
-  };
-  // (1) incident vertices inside the reference rectangle
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (fabs(U[k]) <= e1 && fabs(V[k]) <= e2) out(U[k], V[k], W[k]);
-  // (2) reference corners inside the incident quad (projected along nref), w on the incident plane
-  const T det = a1u * a2v - a2u * a1v;
-  const T ia = a1w * a2v - a2w * a1v, ib = a1u * a2w - a2u * a1w;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const T cu_ = sx[k] * e1, cv_ = sy[k] * e2;
-    bool in = det != T(0);
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int m1 = (m + 1) & 3;
-      T cr = (U[m1] - U[m]) * (cv_ - V[m]) - (V[m1] - V[m]) * (cu_ - U[m]);
-      in = in && (det >= T(0) ? cr > T(0) : cr < T(0));
-    }
-    if (in) out(cu_, cv_, cw + (ia * (cu_ - cu) + ib * (cv_ - cv)) / det);
-  }
-  // (3) proper crossings of incident edges with the rectangle's sides
-#pragma unroll
-  for (int m = 0; m < 4; m++) {
-    const int m1 = (m + 1) & 3;
-#pragma unroll
-    for (int sd = 0; sd < 4; sd++) {
-      const bool onu = sd < 2;
-      const T ss = (sd & 1) ? T(-1) : T(1);
-      const T e = onu ? e1 : e2;
-      const T dp = e - ss * (onu ? U[m] : V[m]);
-      const T dq = e - ss * (onu ? U[m1] : V[m1]);
-      if ((dp > T(0) && dq < T(0)) || (dp < T(0) && dq > T(0))) {
-        const T f = dp / (dp - dq);
-        const T xu = U[m] + (U[m1] - U[m]) * f, xv = V[m] + (V[m1] - V[m]) * f, xw = W[m] + (W[m1] - W[m]) * f;
-        if (onu ? fabs(xv) <= e2 : fabs(xu) < e1) out(xu, xv, xw);
-      }
-    }
+  for (int c = 0; c < 24; c++) {
+    T u, v, w;
+    if (bb_face_candidate(F, c, u, v, w) && !(w > T(0))) bb_face_emit(F, u, v, w, emit);
   }
 }
 
@@ -1098,8 +1145,9 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
 // box-box pairs with the SAT spread over the wave: 4 pairs per pass, lanes 16 p .. 16 p + 14 evaluate axis
 // LANE & 15 of pair p (bb_axis: the serial loop's arithmetic), the group's separation test by ballot, the best
 // face / edge axis by a DPP row minimum (first axis on ties, as the serial strict '<' keeps), the winner's axis and
-// distance fetched by ds_bpermute; lane 16 p then builds the contacts (np_box_box_finish).  A pass costs one axis
-// plus one clipping instead of 15 axes plus the clipping on one lane.
+// distance fetched by ds_bpermute; then a face contact's 24 clipping candidates are spread over the pair's 16 lanes
+// (bb_face_candidate, numbered by a ballot prefix) and an edge contact is built on lane 16 p.  A pass costs one
+// axis and two candidates per lane instead of 15 axes and 24 candidates on one lane.
 template <int CTRL>
 __device__ __forceinline__ double dpp_row(double x) {
   return dpp_f64<CTRL>(x, x);
@@ -1168,10 +1216,30 @@ __device__ __forceinline__ void narrow_bb_parallel(const Model<T>& M, const Ws<T
     sat.edge_u = V3<NP>{__shfl(u.x, el), __shfl(u.y, el), __shfl(u.z, el)};
     sat.edge_s = __shfl(sd, el);
     sat.best_edge = eo;
-    if (live && ax == 0 && !sep) {
-      const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
-      Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
-      np_box_box_finish(p1, R1, h1, p2, R2, h2, sat, emit);
+    const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
+    Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
+    const bool edge = sat.edge_id >= 0 && sat.best_edge < NP(0.95) * sat.best_face;
+    if (live && !sep && edge && ax == 0) np_box_box_finish(p1, R1, h1, p2, R2, h2, sat, emit);  // one point
+    // face contact: candidates c = ax and 16 + ax (ax < 8) of the serial order on the pair's 16 lanes; the k-th
+    // contact in that order (rank by ballot prefix) takes index k within the pair, as the serial loop numbers them
+    bool f0 = false, f1 = false;
+    NP u0 = 0, v0 = 0, w0 = 0, u1 = 0, v1 = 0, w1 = 0;
+    BBFace<NP> F;
+    if (live && !sep && !edge) {
+      F = bb_face_setup(p1, R1, h1, p2, R2, h2, sat);
+      f0 = bb_face_candidate(F, ax, u0, v0, w0) && !(w0 > NP(0));
+      f1 = ax < 8 && bb_face_candidate(F, 16 + ax, u1, v1, w1) && !(w1 > NP(0));
+    }
+    const uint32_t g0 = (uint32_t)(__ballot(f0) >> (16 * grp)) & 0xFFFFu;
+    const uint32_t g1 = (uint32_t)(__ballot(f1) >> (16 * grp)) & 0xFFu;
+    const uint32_t mk = g0 | (g1 << 16);
+    if (f0) {
+      emit.sub = __popc(mk & ((1u << ax) - 1u));
+      bb_face_emit(F, u0, v0, w0, emit);
+    }
+    if (f1) {
+      emit.sub = __popc(mk & ((1u << (16 + ax)) - 1u));
+      bb_face_emit(F, u1, v1, w1, emit);
     }
   }
 }
