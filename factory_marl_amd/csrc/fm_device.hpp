@@ -507,6 +507,14 @@ struct Ws {
       }                                                            \
     }                                                              \
   } while (0)
+template <typename T, typename DIM>
+__device__ constexpr bool dense_mfma_chol();
+// narrowphase split of the compile-time scenes without the dense Cholesky (whose sub-phase slots it borrows):
+// PH_CHDIAG = geom-pair expansion, PH_CHPANEL = sphere / plane pairs, PH_CHTRAIL = box-box pairs
+#define NPMARK(k)                                                       \
+  do {                                                                  \
+    if constexpr (DIM::fixed && !dense_mfma_chol<T, DIM>()) PMARK(k);   \
+  } while (0)
 
 // ------------------------------------------------------------------------------------------------
 // tree / dof helpers
@@ -1474,8 +1482,10 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     nsurv += __popcll(b2m);
     nbb += __popcll(bbm);
     SYNC();
+    NPMARK(PH_CHDIAG);  // geom-pair expansion
     if (nsurv >= WAVE) {
       narrow_batch(M, w, gs, WAVE);
+      NPMARK(PH_CHPANEL);
       const bool mv = LANE + WAVE < nsurv;
       uint32_t t = mv ? gs[LANE + WAVE] : 0u;
       SYNC();
@@ -1485,6 +1495,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     }
     if (nbb >= WAVE) {
       narrow_batch(M, w, gsb, WAVE);
+      NPMARK(PH_CHTRAIL);
       const bool mv = LANE + WAVE < nbb;
       uint32_t t = mv ? gsb[LANE + WAVE] : 0u;
       SYNC();
@@ -1493,13 +1504,16 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
       SYNC();
     }
   }
+  NPMARK(PH_CHDIAG);
   if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
+  NPMARK(PH_CHPANEL);
   if (nbb > 0) {
     if (nbb <= 8 && !(M.dbg_flags & 4))
       narrow_bb_parallel(M, w, gsb, nbb);
     else
       narrow_batch(M, w, gsb, nbb);
   }
+  NPMARK(PH_CHTRAIL);
   SYNC();
   PMARK(PH_CNARROW);
   // 5. sort the staged contacts by key into the contact slots
