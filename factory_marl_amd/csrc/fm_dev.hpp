@@ -445,6 +445,25 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   return x;
 }
 
+// inclusive prefix maximum of an int over the wave (the wave_incl_scan sequence with max)
+__device__ __forceinline__ int wave_incl_max(int x) {
+  const int lane = (int)threadIdx.x, rl = lane & 15;
+  int t;
+  t = dpp_i32<0x111>(x);
+  if (rl >= 1) x = x > t ? x : t;
+  t = dpp_i32<0x112>(x);
+  if (rl >= 2) x = x > t ? x : t;
+  t = dpp_i32<0x114>(x);
+  if (rl >= 4) x = x > t ? x : t;
+  t = dpp_i32<0x118>(x);
+  if (rl >= 8) x = x > t ? x : t;
+  t = dpp_i32<0x142>(x);
+  if ((lane & 31) >= 16) x = x > t ? x : t;
+  t = dpp_i32<0x143>(x);
+  if (lane >= 32) x = x > t ? x : t;
+  return x;
+}
+
 template <typename T>
 struct StepParams {
   Model<T> M;

@@ -1434,21 +1434,28 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   uint32_t* gs = w.gsurv();
   uint32_t* gsb = gs + 2 * WAVE;
   int nsurv = 0, nbb = 0;
+  // the hit entry owning geom pair e (the last entry whose first index is <= e): entries starting in the pass mark
+  // their lane, an inclusive prefix maximum over the wave fills the lanes in between (starts are strictly
+  // increasing: every hit pair expands to >= 1 geom pair), and the pass's last owner carries into the next
+  int* mark = misc + 16;  // [64] scratch of the collision phase
+  int carry = 0;
   for (int e0 = 0; e0 < total; e0 += WAVE) {
     const int e = e0 + LANE;
     bool ok = false;
     uint32_t pk = 0;
     int pc = 0;
+    mark[LANE] = -1;
+    SYNC();
+    for (int q = LANE; q < nsp; q += WAVE) {
+      const int st = (int)(sp[q] >> 16);
+      if (st >= e0 && st < e0 + WAVE) mark[st - e0] = q;
+    }
+    SYNC();
+    int own = wave_incl_max(mark[LANE]);
+    own = own > carry ? own : carry;
+    carry = __builtin_amdgcn_readlane(own, WAVE - 1);
     if (e < total) {
-      int lo = 0, hi = nsp - 1;
-      while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if ((int)(sp[mid] >> 16) <= e)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      const uint32_t bp = sp[lo];
+      const uint32_t bp = sp[own];
       const int x = bp & 255, y = (bp >> 8) & 255;
       const int r = e - (int)(bp >> 16);
       const int ngy = cbi[4 * y + 3];

@@ -21,5 +21,7 @@ timeout -k 10 200 python tools/phase_profile.py --precision fp32 > $O/phase_fp32
 timeout -k 10 200 python tools/phase_profile.py --precision fp64 > $O/phase_fp64.json 2>> $O/phase.err || { echo "PHASE64 FAILED"; tail $O/phase.err; exit 1; }
 timeout -k 10 300 python -u tools/phase_profile.py --steps 3 --arms 4 --objects 16 --env-class PauseIKToggleEnv --preroll 60 > $O/phase_fp32_4x16.json 2>> $O/phase.err || { echo "PHASE416 FAILED"; tail $O/phase.err; exit 1; }
 timeout -k 10 300 python -u tools/phase_profile.py --steps 5 --arms 2 --objects 8 > $O/phase_fp32_2x8.json 2>> $O/phase.err || { echo "PHASE28 FAILED"; tail $O/phase.err; exit 1; }
+timeout -k 10 400 python bench.py --workload config4 --steps 4 --warmup 1 --preroll 10 --no-cpu-baseline > $O/bench_config4_1gpu.json 2> $O/bench_c4.err || { echo "BENCH c4 FAILED"; tail $O/bench_c4.err; exit 1; }
+cat $O/bench_config4_1gpu.json
 find $O -name "*kernel_stats.csv" | head -3
 echo MEASURE_OK
