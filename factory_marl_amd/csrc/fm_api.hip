@@ -182,6 +182,8 @@ static Model<T> make_model(const fm_handle* h) {
   M.dbg_flags = (cl && cl[0] == '1') ? 1 : ((cl && cl[0] == '2') ? 2 : 0);
   const char* sb = getenv("FM_SERIAL_BOXBOX");  // experiment switch: one lane per box-box pair throughout
   if (sb && sb[0] == '1') M.dbg_flags |= 4;
+  const char* nm = getenv("FM_NO_MIDCACHE");  // experiment switch: the midphase list rebuilt at every substep
+  if (nm && nm[0] == '1') M.dbg_flags |= 8;
   return M;
 }
 

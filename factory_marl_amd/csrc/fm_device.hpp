@@ -1350,7 +1350,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   T infl = T(0);
   if constexpr (DIM::midcache) {
     bool moved = false;
-    const int ok = misc[MISC_MC_OK];
+    const int ok = misc[MISC_MC_OK] && !(M.dbg_flags & 8);  // FM_NO_MIDCACHE=1: rebuild every substep
     for (int b = LANE; b < dm.ncb; b += WAVE) {
       const T* o = w.cbw() + 8 * b;
       const T* p0 = w.mpos() + 3 * b;
