@@ -69,15 +69,16 @@ def test_parallel_box_box_is_exact():
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 def test_parallel_box_box_fp64_to_rounding():
     """fp64: the two code paths are inlined into different contexts and the compiler contracts a few multiply-adds
-    differently, so they agree to float64 rounding rather than bit for bit (one env-step from 256 states)"""
+    differently, so they agree to float64 rounding rather than bit for bit (40 env-steps of 256 arenas: measured
+    3.2e-11 relative, tools/boxbox_probe.py)"""
     import parity_util as pu
     from factory_marl_amd import state as st
 
-    a, b = _run(2, 4, 256, 1, "FM_SERIAL_BOXBOX", precision="fp64")
+    a, b = _run(2, 4, 256, 40, "FM_SERIAL_BOXBOX", precision="fp64")
     worst = max(max(m.max() for m in pu.state_err(2, 4, st.unpack(2, 4, a[i])[0], st.unpack(2, 4, b[i])[0]))
                 for i in range(len(a)))
-    print(f"parallel vs serial box-box, fp64, one env-step: worst relative state difference {worst:.2e}")
-    assert worst <= 1e-10
+    print(f"parallel vs serial box-box, fp64, 40 env-steps: worst relative state difference {worst:.2e}")
+    assert worst <= 1e-9
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
