@@ -120,6 +120,7 @@ void or_make_constraint(const or_model* m, or_data* d);
 void or_step1(const or_model* m, or_data* d);
 void or_step2(const or_model* m, or_data* d);
 void or_set_accel_noise(double amp, uint64_t seed); /* sensitivity probe only (tools/fp32_floor.py) */
+void or_set_solver_tol(double tol);                /* Newton tolerance study only (tools/tolerance_floor.py) */
 void or_forward(const or_model* m, or_data* d); /* step1 + acceleration stage, no integration */
 void or_jac_point(const or_model* m, const or_data* d, int body, const double p[3], double* jacp, double* jacr);
 void or_contact_force(const or_model* m, const or_data* d, int i, double out[6]);

@@ -97,7 +97,7 @@ def _bind(L, real):
             "or_d_efc_aref": (DP, [P]), "or_d_efc_J": (DP, [P]), "or_d_stage_fwd": (DP, [P, P, I]),
             "or_env_import": (None, [P, P, P, P]),
             "or_batch_bench": (D, [I, I, I, I, I, U64, P]),
-            "or_set_accel_noise": (None, [D, U64]),
+            "or_set_accel_noise": (None, [D, U64]), "or_set_solver_tol": (None, [D]),
             "or_ik_arm_init_flat": (None, [P, P]), "or_ik_arm_reset_flat": (None, [P, P]),
             "or_ik_plan_flat": (I, [I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
             "or_ik_finish_flat": (None, [P, P, I, P, I, P]),

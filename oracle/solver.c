@@ -30,6 +30,9 @@
 #define OR_SOLVER_TOL 1e-12 /* liboracle_f32.so (fp32 floor study) overrides it */
 #endif
 #define OR_SOLVER_ITER 100
+/* the tolerance in use: OR_SOLVER_TOL unless a study sets another (or_set_solver_tol, tools/tolerance_floor.py) */
+static double or_solver_tol = OR_SOLVER_TOL;
+void or_set_solver_tol(double tol) { or_solver_tol = tol > 0 ? tol : OR_SOLVER_TOL; }
 #ifndef OR_PYR_KSCALE
 #define OR_PYR_KSCALE(mu) (4.0 * (mu) * (mu)) /* pyramid edges: aref position stiffness K / this (header comment) */
 #endif
@@ -229,7 +232,7 @@ void or_solve(const or_model* m, or_data* d) {
     }
     double gn = 0;
     for (int i = 0; i < nv; i++) gn += g[i] * g[i];
-    if (scale * sqrt(gn) < OR_SOLVER_TOL) break;
+    if (scale * sqrt(gn) < or_solver_tol) break;
     or_cholesky_env(H, nv, nz);
     for (int i = 0; i < nv; i++) dir[i] = -g[i];
     or_chol_solve_env(H, nv, nz, dir);
@@ -296,7 +299,7 @@ void or_solve(const or_model* m, or_data* d) {
     double newcost = cost_at(m, d, a, jar, Ma);
     double improvement = scale * (cost - newcost);
     cost = newcost;
-    if (improvement < OR_SOLVER_TOL) {
+    if (improvement < or_solver_tol) {
       it++;
       break;
     }

@@ -3,7 +3,7 @@
 solver setting, one JSON line per trajectory (tests/parity_util.summary + the setting).
 
 usage: FACTORYSIM_LIB=path python tools/parity_sweep.py --prec fp32 [--tol 1e-9] [--tag name]
-           [--traj A,K,T,seed[,EnvClass] ...]   (default: 2,4,96,7  2,4,300,21  2,8,300,5  2,10,250,9)
+           [--traj A,K,T,seed[,EnvClass[,oracle_tol]] ...]   (default: 2,4,96,7  2,4,300,21  2,8,300,5  2,10,250,9)
 Trajectories are cached as .npz under gpurun_out/traj/ (or $FM_TRAJ_CACHE: a cache made in the container travels
 with the tree) so several processes share one oracle rollout.
 """
@@ -24,10 +24,16 @@ from oracle import pyoracle as po  # noqa: E402  (checker)
 
 
 def load_traj(A, K, T, seed, env_class="AllFullRLProgressRewardEnv",
-              cache=os.environ.get("FM_TRAJ_CACHE", os.path.join(ROOT, "gpurun_out", "traj"))):
+              cache=os.environ.get("FM_TRAJ_CACHE", os.path.join(ROOT, "gpurun_out", "traj")), oracle_tol=0.0):
+    """oracle_tol > 0: the expected outputs come from an oracle whose Newton stops at that tolerance (MuJoCo's
+    default 1e-8), stepped from the same states (tools/tolerance_floor.py --make-traj writes those files)"""
     os.makedirs(cache, exist_ok=True)
     tag = "" if env_class == "AllFullRLProgressRewardEnv" else "_" + env_class
+    if oracle_tol > 0:
+        tag += f"_tol{oracle_tol:g}"
     f = os.path.join(cache, f"traj_{A}_{K}_{T}_{seed}{tag}.npz")
+    if oracle_tol > 0 and not os.path.exists(f):
+        raise FileNotFoundError(f + " (make it with tools/tolerance_floor.py --make-traj)")
     if os.path.exists(f):
         z = np.load(f)
         meta = json.load(open(f[:-4] + ".json"))
@@ -57,9 +63,10 @@ def main():
     for spec in args.traj:
         f = spec.split(",")
         A, K, T, seed = (int(x) for x in f[:4])
-        env_class = f[4] if len(f) > 4 else "AllFullRLProgressRewardEnv"
+        env_class = f[4] if len(f) > 4 and f[4] else "AllFullRLProgressRewardEnv"
+        otol = float(f[5]) if len(f) > 5 else 0.0
         t0 = time.time()
-        traj = load_traj(A, K, T, seed, env_class)
+        traj = load_traj(A, K, T, seed, env_class, oracle_tol=otol)
         t1 = time.time()
         r = pu.compare(traj, args.prec, A, K, env_class, solver_tolerance=args.tol, solver_iterations=args.iters)
         s = pu.summary(r)
