@@ -41,6 +41,30 @@ def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights
     return np.stack(recs), np.stack(acts), outs
 
 
+def restep_at_tolerance(oracle, A, K, trajectory, tol):
+    """the same states and actions, stepped by an oracle whose Newton stops at `tol` (MuJoCo's default opt.tolerance
+    is 1e-8; the oracle's own is 1e-12): the expected outputs of a MuJoCo-tolerance solve"""
+    from factory_marl_amd import state as st
+
+    recs, acts, _ = trajectory
+    p = oracle.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4))
+    p.reset()
+    L = oracle.lib()
+    outs = []
+    try:
+        for k in range(len(recs)):
+            d, i, r = st.unpack(A, K, recs[k])
+            p.import_state(d, i, r)
+            L.or_set_solver_tol(tol)
+            obs, rew, term, _, info = p.step(acts[k])
+            L.or_set_solver_tol(0.0)
+            d2, i2, r2 = p.export_state()
+            outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
+    finally:
+        L.or_set_solver_tol(0.0)
+    return recs, acts, outs
+
+
 def gpu_env(n, precision, A, K, env_class="AllFullRLProgressRewardEnv", **kw):
     from factory_marl_amd import FactoryVecEnv
 

@@ -52,21 +52,8 @@ def make_traj(tol, A, K, T, seed_actions, cache):
     """the parity sweep's trajectory (parity_util.rollout: states and actions of the 1e-12 oracle) with the
     expected outputs of the tolerance-`tol` oracle stepped from each state"""
     import parity_util as pu
-    from factory_marl_amd import state as st
 
-    recs, acts, _ = pu.rollout(po, A, K, T, seed_actions=seed_actions)
-    p = po.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4))
-    p.reset()
-    L = po.lib()
-    outs = []
-    for k in range(T):
-        d, i, r = st.unpack(A, K, recs[k])
-        p.import_state(d, i, r)
-        L.or_set_solver_tol(tol)
-        obs, rew, term, _, info = p.step(acts[k])
-        L.or_set_solver_tol(0.0)
-        d2, i2, r2 = p.export_state()
-        outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
+    recs, acts, outs = pu.restep_at_tolerance(po, A, K, pu.rollout(po, A, K, T, seed_actions=seed_actions), tol)
     f = os.path.join(cache, f"traj_{A}_{K}_{T}_{seed_actions}_tol{tol:g}.npz")
     np.savez(f, recs=recs, acts=acts, obs=np.stack([o["obs"] for o in outs]),
              reward=np.array([o["reward"] for o in outs]), term=np.array([o["term"] for o in outs]),
