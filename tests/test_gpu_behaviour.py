@@ -48,14 +48,16 @@ def test_saved_policy_return_and_length_match_training_episodes(run):
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-def test_ik_base_policy_against_the_report():
+@pytest.mark.parametrize("A,length,scores", [(2, 208.8, (1.65, 1.17)), (4, 119.74, (1.18, 1.16))])
+def test_ik_base_policy_against_the_report(A, length, scores):
+    """report.tex:276-295 (measured here: 2 arms (1.72, 1.70) in 232.7 steps, 4 arms (1.05, 0.95) in 109.6)"""
     import behaviour
 
-    out = behaviour.base(types.SimpleNamespace(A=2, arenas=512, episodes=0, precision="fp32"))
+    out = behaviour.base(types.SimpleNamespace(A=A, arenas=512, episodes=0, precision="fp32"))
     par = out["parallel"]
     print(json.dumps(par))
     assert par["finished"] == 512
     score = par["scores0"]["mean"] + par["scores1"]["mean"]
-    assert abs(par["length_t"]["mean"] / 208.8 - 1) <= 0.15, par["length_t"]
-    assert abs(score / (1.65 + 1.17) - 1) <= 0.30, score
+    assert abs(par["length_t"]["mean"] / length - 1) <= 0.15, par["length_t"]
+    assert abs(score / sum(scores) - 1) <= 0.30, score
     assert np.isfinite(score)
