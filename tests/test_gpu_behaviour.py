@@ -30,7 +30,9 @@ def _have_gpu():
 
 
 # run -> (band on the mean return, band on the mean length), relative to the run's ep_info_buffer means
-POLICY_BANDS = {"rk5rxnav": (0.06, 0.05), "r666unuv": (0.06, 0.05)}
+# (measured, 512 arenas: rk5rxnav r -3.1 % l -1.6 %; r666unuv -3.0 % / -1.8 %; xfwgqibb +2.1 % / -2.7 %; y6lp1j7k
+# +13.7 % / +5.5 % -- the toggle runs' 100-episode buffers carry standard errors of 6-9 % of their means)
+POLICY_BANDS = {"rk5rxnav": (0.06, 0.05), "r666unuv": (0.06, 0.05), "xfwgqibb": (0.15, 0.10), "y6lp1j7k": (0.25, 0.15)}
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
