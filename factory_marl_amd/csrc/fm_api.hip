@@ -184,6 +184,8 @@ static Model<T> make_model(const fm_handle* h) {
   if (sb && sb[0] == '1') M.dbg_flags |= 4;
   const char* nm = getenv("FM_NO_MIDCACHE");  // experiment switch: the midphase list rebuilt at every substep
   if (nm && nm[0] == '1') M.dbg_flags |= 8;
+  const char* na = getenv("FM_NO_ARROW");  // experiment switch: no block-parallel arrowhead Cholesky
+  if (na && na[0] == '1') M.dbg_flags |= 16;
   return M;
 }
 

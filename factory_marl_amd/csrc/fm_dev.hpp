@@ -119,7 +119,8 @@ struct Model {
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
-  int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one
+  int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one;
+                             // bit 2 serial box-box, bit 3 no midphase cache, bit 4 no arrowhead Cholesky
                              // instead of the dense matrix-core one for runtime-dims fp32 (FM_CHOL_LDS=2); bit 2 = the
                              // serial box-box narrowphase (FM_SERIAL_BOXBOX=1); bit 3 = no midphase reuse
                              // (FM_NO_MIDCACHE=1)

@@ -2393,10 +2393,30 @@ __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_
 //  * Tree-block sparsity: H couples two trees only through a contact between them.  The coupling graph (plus
 //    the fill-in of this elimination order) comes from the tree->contact masks; a pivot updates only the row
 //    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
+//  * Arrowhead fast path (chol_arrow_rl): when no contact couples two trees other than the belt -- the common
+//    substep -- H in this order is block diagonal with a belt border, and the tree blocks factor independently.
+template <typename T, typename DIM>
+__device__ __forceinline__ void chol_arrow_rl(const T* H, const double* g, T* dir);
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
                                                T* dir) {
   constexpr int NV = DIM::nv, KK = DIM::K, AA = DIM::A, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
+  if (!(M.dbg_flags & 16)) {
+    // arrowhead test: no contact shared by two trees other than the belt (tree 0); uniform, a scalar branch
+    uint64_t any = 0, both = 0;
+#pragma unroll
+    for (int t = 1; t < NT; t++) {
+      const uint64_t m = w.tmask()[t];
+      const uint64_t mt = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
+      both |= any & mt;
+      any |= mt;
+    }
+    if (both == 0) {
+      chol_arrow_rl<T, DIM>(H, g, dir);
+      return;
+    }
+  }
   const int j = LANE;
   const int jo = j == NV - 1 ? 0 : j + 1;  // lane j's dof (original numbering)
   T col[NV];
@@ -2489,6 +2509,99 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
     if (j < k) acc2 -= col[k] * dinv * xk;
   }
   if (j < NV) dir[jo] = x;
+  SYNC();
+}
+
+// Arrowhead Cholesky (chol_sparse_rl's fast path).  No contact couples two trees other than the belt, so in the
+// elimination order (cubes, arms, belt last) H is block diagonal -- one 6x6 block per cube, one 9x9 per arm --
+// plus the belt's border row, and there is no fill-in outside the blocks and the border.  All blocks take their
+// s-th pivot in the same step: 9 pivot steps instead of NV - 1, and 9 + 9 substitution steps instead of 2 NV.
+//  * Lane j (position j, j < NV - 1) keeps its column's rows of its own block (local index, so every lane uses
+//    the same registers) and its belt row `bel` (= H[belt][j] by symmetry); the pivot and the multipliers of its
+//    block come from the block's lanes by ds_bpermute.
+//  * The belt lane takes no part in the block steps: its column is the other lanes' `bel`; its diagonal and its
+//    forward-substitution row are accumulated afterwards in pivot order by a v_readlane chain.
+// Every entry sees the operations of chol_sparse_rl in the same order (the updates it skips are products with
+// exact zeros), so the factor and the direction are bit-identical to it.
+template <typename T, typename DIM>
+__device__ __forceinline__ void chol_arrow_rl(const T* H, const double* g, T* dir) {
+  constexpr int NV = DIM::nv, A0 = 1 + 6 * DIM::K, NB = NV - 1;
+  static_assert(NV <= WAVE, "one lane per position");
+  const int j = LANE;
+  const bool blk = j < NB;                   // a block lane (not the belt, not idle)
+  const int jo = j == NV - 1 ? 0 : j + 1;    // lane j's dof (original numbering)
+  const int ps = j < A0 - 1 ? (j / 6) * 6 : A0 - 1 + ((j - (A0 - 1)) / 9) * 9;  // own block's first position
+  const int pn = j < A0 - 1 ? 6 : 9;         // own block's size
+  const int jl = j - ps;                     // local index
+  T loc[9];
+#pragma unroll
+  for (int ii = 0; ii < 9; ii++) loc[ii] = (blk && ii < pn) ? H[(ps + ii + 1) * NV + jo] : T(0);
+  T bel = blk ? H[jo] : T(0);  // row 0 (the belt) of column jo
+  const T hbb = H[0];
+  SYNC();
+  const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
+  T dinv = T(1), lbelt = T(0);
+  static_for<0, 9>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    const bool act = blk && s < pn;  // the block has a pivot in this step
+    const int p = (ps + s) & (WAVE - 1);
+    T d = __shfl(loc[s], p);
+    d = d > tiny ? d : tiny;
+    const T ri = T(1) / sqrt(d);
+    const T lj = loc[s] * ri;           // L[j][k] (j >= k)
+    const T lb = __shfl(bel, p) * ri;   // L[belt][k]
+    if (act && jl == s) {
+      dinv = ri;
+      lbelt = lb;
+    }
+    if (act && jl >= s) loc[s] = lj;
+    T lv[9];
+#pragma unroll
+    for (int ii = s + 1; ii < 9; ii++) lv[ii] = __shfl(lj, (ps + ii) & (WAVE - 1));  // L[i][k], i in the block
+    if (act && jl > s) {
+#pragma unroll
+      for (int ii = s + 1; ii < 9; ii++)
+        if (ii < pn) loc[ii] -= lv[ii] * lj;
+      bel -= lb * lj;
+    }
+  });
+  // belt pivot: its diagonal minus its row of L, in pivot order
+  T db = hbb;
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    const T x = readlane(lbelt, k);
+    db -= x * x;
+  }
+  db = db > tiny ? db : tiny;
+  const T rib = T(1) / sqrt(db);
+  // forward: L y = -g
+  T acc = blk ? (T)-g[jo] : T(0);
+  T y = T(0);
+  static_for<0, 9>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    const bool act = blk && s < pn;
+    const T yk = __shfl(acc * dinv, (ps + s) & (WAVE - 1));
+    if (act && jl == s) y = yk;
+    if (act && jl > s) acc -= loc[s] * yk;
+  });
+  T accb = (T)-g[0];
+#pragma unroll
+  for (int k = 0; k < NB; k++) accb -= readlane(lbelt, k) * readlane(y, k);
+  const T yb = accb * rib;
+  // backward: L' x = y, the belt first
+  const T xb = yb * rib;
+  T acc2 = y;
+  if (blk) acc2 -= bel * dinv * xb;
+  T x = T(0);
+  static_for<0, 9>([&](auto sc) {
+    constexpr int s = 8 - decltype(sc)::value;
+    const bool act = blk && s < pn;
+    const T xk = __shfl(acc2 * dinv, (ps + s) & (WAVE - 1));
+    if (act && jl == s) x = xk;
+    if (act && jl < s) acc2 -= loc[s] * dinv * xk;
+  });
+  if (blk) dir[jo] = x;
+  if (j == NV - 1) dir[0] = xb;
   SYNC();
 }
 
