@@ -186,6 +186,11 @@ static Model<T> make_model(const fm_handle* h) {
   if (nm && nm[0] == '1') M.dbg_flags |= 8;
   const char* na = getenv("FM_NO_ARROW");  // experiment switch: no block-parallel arrowhead Cholesky
   if (na && na[0] == '1') M.dbg_flags |= 16;
+  if (na && na[0] == '2') M.dbg_flags |= 32;  // arrowhead factor of the LDS-assembled Hessian
+  const char* ns = getenv("FM_NO_SCATTER");  // experiment switch: per-dof gather of J' f instead of the scatter
+  if (ns && ns[0] == '1') M.dbg_flags |= 64;
+  const char* sf = getenv("FM_SERIAL_FK");  // experiment switch: arm kinematics / RNE on one lane per arm
+  if (sf && sf[0] == '1') M.dbg_flags |= 128;
   return M;
 }
 

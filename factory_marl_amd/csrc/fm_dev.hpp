@@ -119,11 +119,13 @@ struct Model {
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
-  int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one;
-                             // bit 2 serial box-box, bit 3 no midphase cache, bit 4 no arrowhead Cholesky
+  int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one
                              // instead of the dense matrix-core one for runtime-dims fp32 (FM_CHOL_LDS=2); bit 2 = the
                              // serial box-box narrowphase (FM_SERIAL_BOXBOX=1); bit 3 = no midphase reuse
-                             // (FM_NO_MIDCACHE=1)
+                             // (FM_NO_MIDCACHE=1); bit 4 = no arrowhead Cholesky (FM_NO_ARROW=1); bit 5 = the
+                             // arrowhead factor of the LDS-assembled Hessian (FM_NO_ARROW=2); bit 6 = the per-dof
+                             // gather of J' f instead of the scatter (FM_NO_SCATTER=1); bit 7 = the serial arm
+                             // kinematics (FM_SERIAL_FK=1)
 };
 
 template <typename T>

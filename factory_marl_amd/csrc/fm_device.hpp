@@ -1876,6 +1876,253 @@ __device__ __forceinline__ void arm_rne_back(const Model<T>& M, const Ws<T, DIM>
   }
 }
 
+// DPP moves inside rows of 16 lanes (dpp_row): row_shr:n (lane l reads lane l - n) and row_shl:n (lane l reads
+// l + n); a lane whose source lies outside its row keeps its own value.  Full wave active at every call site.
+enum { DPP_SHR = 0x110, DPP_SHL = 0x100 };
+
+// Arm kinematics + RNE of the physics substep (arm_chain<DYN> + arm_body_post<DYN> + arm_rne_back) as scans
+// over the kinematic chain instead of one serial lane per arm: arm a's body b on lane 16 a + b (one DPP row per
+// arm, A <= 4).  The chain link1..7, gripper base, left plate occupies lanes b = 0..8 (each body's parent is the
+// lane before); the right plate (b = 9) hangs off the gripper base (b = 7) and joins after each scan.
+//  * poses: every lane builds its body's transform relative to its parent (hinge: R_body Rz(q); plate: the slide
+//    along the local x axis), then a Hillis-Steele scan of rigid-transform products over row_shr 1, 2, 4, 8 gives
+//    the pose relative to the arm base; one product with the base gives the world pose (a reassociation of the
+//    serial chain's products);
+//  * velocities (flg_acc = 0): angular velocity, angular acceleration and origin acceleration are sums along the
+//    chain of per-body terms (a hinge adds axis * qdot to w and (w_parent x axis) qdot to the angular
+//    acceleration; every body adds alpha_parent x r + w_parent x (w_parent x r), a plate also
+//    2 (w_parent x axis) qdot), each a prefix-sum scan once its terms' parent values are known;
+//  * the per-body com / world inertia / RNE force and moment of arm_body_post on the same lane, then the RNE
+//    backward sums over the subtrees (both plates folded into the gripper base, a row_shl suffix scan) and the
+//    bias forces of the 9 dofs.
+// Outputs to LDS as the serial path: body poses, joint axes / anchors, site, coms, world inertias, qfrc_bias.
+template <typename T, typename DIM>
+__device__ __forceinline__ void arm_fk_scan(const Model<T>& M, const Ws<T, DIM>& w) {
+  const DIM dm(M.dm);
+  const int A = dm.A, K = dm.K;
+  const int arm = LANE >> 4, b = LANE & 15;
+  const bool on = arm < A && b < 10;
+  const int bb = on ? b : 0, aa = on ? arm : 0;  // clamped for the table loads
+  const T* bl = M.body + 32 * bb;
+  const T* base = M.arm_base + 12 * aa;
+  const int d = bb < 7 ? bb : (bb == 7 ? -1 : bb - 1);  // the body's joint: hinge b, none, slide dof 7 / 8
+  const T qj = d >= 0 ? w.q()[1 + 7 * K + 9 * aa + d] : T(0);
+  const T vj = d >= 0 ? w.v()[1 + 6 * K + 9 * aa + d] : T(0);
+  T R[9], p[3];
+  {
+    T BR[9], lp[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) BR[k] = bl[3 + k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) lp[k] = bl[k];
+    T sn, cs;
+    sincos_t(bb < 7 ? qj : T(0), &sn, &cs);
+    const bool hinge = bb < 7, slide = bb >= 8;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      R[3 * r + 0] = hinge ? BR[3 * r + 0] * cs + BR[3 * r + 1] * sn : BR[3 * r + 0];
+      R[3 * r + 1] = hinge ? -BR[3 * r + 0] * sn + BR[3 * r + 1] * cs : BR[3 * r + 1];
+      R[3 * r + 2] = BR[3 * r + 2];
+      p[r] = slide ? lp[r] + BR[3 * r] * qj : lp[r];
+    }
+  }
+  // X = (Ra, pa) o X
+  auto compose = [&](const T* Ra, const T* pa) {
+    T Rn[9], pn[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) Rn[3 * i + j] = Ra[3 * i] * R[j] + Ra[3 * i + 1] * R[3 + j] + Ra[3 * i + 2] * R[6 + j];
+      pn[i] = pa[i] + Ra[3 * i] * p[0] + Ra[3 * i + 1] * p[1] + Ra[3 * i + 2] * p[2];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = Rn[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) p[k] = pn[k];
+  };
+  static_for<0, 4>([&](auto rc) {
+    constexpr int s = 1 << decltype(rc)::value;
+    T Ra[9], pa[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) Ra[k] = dpp_row<DPP_SHR | s>(R[k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) pa[k] = dpp_row<DPP_SHR | s>(p[k]);
+    if (b >= s && b <= 8) compose(Ra, pa);
+  });
+  {
+    T Ra[9], pa[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) Ra[k] = dpp_row<DPP_SHR | 2>(R[k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) pa[k] = dpp_row<DPP_SHR | 2>(p[k]);
+    if (b == 9) compose(Ra, pa);  // right plate: gripper base o right plate
+  }
+  const T p0[3] = {base[0], base[1], base[2]};
+  {
+    T Rb[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) Rb[k] = base[3 + k];
+    compose(Rb, p0);
+  }
+  // joint axis (hinge: local z; slide: local x) and anchor
+  const T ax[3] = {bb < 7 ? R[2] : (bb >= 8 ? R[0] : T(0)), bb < 7 ? R[5] : (bb >= 8 ? R[3] : T(0)),
+                   bb < 7 ? R[8] : (bb >= 8 ? R[6] : T(0))};
+  if (on) {
+    T* bpos = w.bpos() + 30 * arm + 3 * b;
+    T* bR = w.bR() + 90 * arm + 9 * b;
+#pragma unroll
+    for (int k = 0; k < 3; k++) bpos[k] = p[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) bR[k] = R[k];
+    if (d >= 0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        w.dax()[27 * arm + 3 * d + k] = ax[k];
+        w.danc()[27 * arm + 3 * d + k] = p[k];
+      }
+    }
+    if (b == 7) {  // between_gripper_plates site (gripper.xml:43)
+      T sp[3];
+      matvec3_c(R, ARM_GRIP_SITE, sp);
+#pragma unroll
+      for (int k = 0; k < 3; k++) w.site()[3 * arm + k] = p[k] + sp[k];
+    }
+  }
+  // prefix sums along the chain (lanes 0..8), the right plate takes the gripper base's value plus its own term
+  auto chain_sum = [&](T* x) {
+    static_for<0, 4>([&](auto rc) {
+      constexpr int s = 1 << decltype(rc)::value;
+      T t[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) t[k] = dpp_row<DPP_SHR | s>(x[k]);
+      if (b >= s && b <= 8) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) x[k] += t[k];
+      }
+    });
+    T t[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) t[k] = dpp_row<DPP_SHR | 2>(x[k]);
+    if (b == 9) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) x[k] += t[k];
+    }
+  };
+  // the parent's value of x (the arm base's `root` for b = 0)
+  auto parent = [&](const T* x, const T* root, T* out) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const T t1 = dpp_row<DPP_SHR | 1>(x[k]), t2 = dpp_row<DPP_SHR | 2>(x[k]);
+      out[k] = b == 0 ? root[k] : (b == 9 ? t2 : t1);
+    }
+  };
+  const T zero3[3] = {T(0), T(0), T(0)};
+  T wv[3] = {bb < 7 ? ax[0] * vj : T(0), bb < 7 ? ax[1] * vj : T(0), bb < 7 ? ax[2] * vj : T(0)};
+  chain_sum(wv);
+  T wp[3];
+  parent(wv, zero3, wp);
+  T wa[3];  // w_parent x axis
+  cross3(wp, ax, wa);
+  T al[3] = {bb < 7 ? wa[0] * vj : T(0), bb < 7 ? wa[1] * vj : T(0), bb < 7 ? wa[2] * vj : T(0)};
+  chain_sum(al);
+  T alp[3], op[3];
+  parent(al, zero3, alp);
+  parent(p, p0, op);
+  T ao[3];
+  {
+    const T r[3] = {p[0] - op[0], p[1] - op[1], p[2] - op[2]};
+    T t1[3], t2[3], t3[3];
+    cross3(wp, r, t1);
+    cross3(alp, r, t2);
+    cross3(wp, t1, t3);
+#pragma unroll
+    for (int k = 0; k < 3; k++) ao[k] = t2[k] + t3[k] + (bb >= 8 ? T(2) * wa[k] * vj : T(0));
+  }
+  chain_sum(ao);
+  // arm_body_post on this lane: com, world inertia, RNE body force / moment about the arm base
+  T F[3], N[3];
+  {
+    T ci[3];
+    matvec3(R, bl + 13, ci);
+    const T com[3] = {p[0] + ci[0], p[1] + ci[1], p[2] + ci[2]};
+    T Ri[9];
+    matmul3(R, bl + 16, Ri);
+    const T I0 = bl[25], I1 = bl[26], I2 = bl[27];
+    T Iw[6];
+    Iw[0] = Ri[0] * Ri[0] * I0 + Ri[1] * Ri[1] * I1 + Ri[2] * Ri[2] * I2;
+    Iw[1] = Ri[3] * Ri[3] * I0 + Ri[4] * Ri[4] * I1 + Ri[5] * Ri[5] * I2;
+    Iw[2] = Ri[6] * Ri[6] * I0 + Ri[7] * Ri[7] * I1 + Ri[8] * Ri[8] * I2;
+    Iw[3] = Ri[0] * Ri[3] * I0 + Ri[1] * Ri[4] * I1 + Ri[2] * Ri[5] * I2;
+    Iw[4] = Ri[0] * Ri[6] * I0 + Ri[1] * Ri[7] * I1 + Ri[2] * Ri[8] * I2;
+    Iw[5] = Ri[3] * Ri[6] * I0 + Ri[4] * Ri[7] * I1 + Ri[5] * Ri[8] * I2;
+    if (on) {
+      T* bcom = w.bcom() + 30 * arm + 3 * b;
+      T* bIw = w.bIw() + 60 * arm + 6 * b;
+#pragma unroll
+      for (int k = 0; k < 3; k++) bcom[k] = com[k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) bIw[k] = Iw[k];
+    }
+    const T mass = bl[12];
+    const T rc[3] = {com[0] - p[0], com[1] - p[1], com[2] - p[2]};
+    T u1[3], u2[3], u3[3];
+    cross3(al, rc, u1);
+    cross3(wv, rc, u2);
+    cross3(wv, u2, u3);
+#pragma unroll
+    for (int k = 0; k < 3; k++) F[k] = (ao[k] + u1[k] + u3[k]) * mass;
+    F[2] += mass * M.grav;
+    const T Iwv[3] = {Iw[0] * wv[0] + Iw[3] * wv[1] + Iw[4] * wv[2], Iw[3] * wv[0] + Iw[1] * wv[1] + Iw[5] * wv[2],
+                      Iw[4] * wv[0] + Iw[5] * wv[1] + Iw[2] * wv[2]};
+    const T Ial[3] = {Iw[0] * al[0] + Iw[3] * al[1] + Iw[4] * al[2], Iw[3] * al[0] + Iw[1] * al[1] + Iw[5] * al[2],
+                      Iw[4] * al[0] + Iw[5] * al[1] + Iw[2] * al[2]};
+    T gy[3];
+    cross3(wv, Iwv, gy);
+    const T cr[3] = {com[0] - p0[0], com[1] - p0[1], com[2] - p0[2]};
+    T mo[3];
+    cross3(cr, F, mo);
+#pragma unroll
+    for (int k = 0; k < 3; k++) N[k] = mo[k] + Ial[k] + gy[k];
+  }
+  // RNE backward: subtree sums of (F, N); the plates fold into the gripper base, then a suffix scan over b <= 7
+  T X[6] = {F[0], F[1], F[2], N[0], N[1], N[2]};
+  {
+    T t1[6], t2[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      t1[k] = dpp_row<DPP_SHL | 1>(X[k]);
+      t2[k] = dpp_row<DPP_SHL | 2>(X[k]);
+    }
+    if (b == 7) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) X[k] += t1[k] + t2[k];
+    }
+  }
+  static_for<0, 3>([&](auto rc) {
+    constexpr int s = 1 << decltype(rc)::value;
+    T t[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) t[k] = dpp_row<DPP_SHL | s>(X[k]);
+    if (b + s <= 7) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) X[k] += t[k];
+    }
+  });
+  if (on && d >= 0) {
+    T tq;
+    if (b < 7) {
+      const T ar[3] = {p[0] - p0[0], p[1] - p0[1], p[2] - p0[2]};
+      T af[3];
+      cross3(ar, X, af);
+      const T tn[3] = {X[3] - af[0], X[4] - af[1], X[5] - af[2]};
+      tq = -dot3(ax, tn);
+    } else {
+      tq = -(ax[0] * F[0] + ax[1] * F[1] + ax[2] * F[2]);
+    }
+    w.pb()[1 + 6 * K + 9 * arm + d] = tq;
+  }
+}
+
 // column of the translational Jacobian of point p on arm body b for arm dof d (0 if not in chain)
 template <typename T, typename DIM>
 __device__ __forceinline__ void arm_jac_col(const Ws<T, DIM>& w, int arm, int b, int d, const T* p, T* col) {
@@ -1931,10 +2178,16 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   const int A = dm.A, K = dm.K, nv = dm.nv;
   T* q = w.q();
   T* v = w.v();
-  // ---- kinematics + RNE (one lane per arm), cubes (one lane per cube)
-  arm_hinge_sincos(M, w);
-  SYNC();
-  if (LANE < A) arm_chain<T, DIM, true>(M, w, LANE);
+  // ---- kinematics + RNE: scans over each arm's chain (arm_fk_scan, A <= 4; FM_SERIAL_FK=1: one lane per arm),
+  // cubes (one lane per cube)
+  const bool fk_scan = dm.A <= 4 && !(M.dbg_flags & 128);
+  if (fk_scan) {
+    arm_fk_scan(M, w);
+  } else {
+    arm_hinge_sincos(M, w);
+    SYNC();
+    if (LANE < A) arm_chain<T, DIM, true>(M, w, LANE);
+  }
   for (int k = LANE; k < K; k += WAVE) {
     T* qq = q + 1 + 7 * k;
     T qu[4] = {qq[3], qq[4], qq[5], qq[6]};
@@ -1966,11 +2219,13 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   }
   if (LANE == 0) w.pb()[0] = -M.belt_damp * v[0];  // belt: damping, no gravity along y
   SYNC();
-  // per-body com / inertia / RNE forces one lane per (arm, body), then the RNE backward sum one lane per arm
-  for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, true>(M, w, e / 10, e % 10);
-  SYNC();
-  if (LANE < A) arm_rne_back(M, w, LANE);
-  SYNC();
+  if (!fk_scan) {
+    // per-body com / inertia / RNE forces one lane per (arm, body), then the RNE backward sum one lane per arm
+    for (int e = LANE; e < 10 * A; e += WAVE) arm_body_post<T, DIM, true>(M, w, e / 10, e % 10);
+    SYNC();
+    if (LANE < A) arm_rne_back(M, w, LANE);
+    SYNC();
+  }
   PMARK(PH_FK);
   // ---- arm mass-matrix blocks, composite-rigid-body style.  Hinge i moves the bodies b >= i; about its anchor
   // p_i their composite mass moment h_i = sum m r and inertia J_i = sum Iw + m (|r|^2 1 - r r'), r = com - p_i
@@ -2395,27 +2650,40 @@ __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_
 //    blocks of trees coupled to its own.  Skipped entries are exact zeros of the dense factorization.
 //  * Arrowhead fast path (chol_arrow_rl): when no contact couples two trees other than the belt -- the common
 //    substep -- H in this order is block diagonal with a belt border, and the tree blocks factor independently.
+template <typename T, typename DIM, bool ASM>
+__device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
+                                              T* dir, int nrow);
+
+// scenes with the register Cholesky on one 64-contact tree-mask word ((2,4), fp32 and fp64)
 template <typename T, typename DIM>
-__device__ __forceinline__ void chol_arrow_rl(const T* H, const double* g, T* dir);
+__device__ constexpr bool arrow_scene() {
+  if constexpr (DIM::fixed)
+    return DIM::MAXC == WAVE && DIM::nv <= 48;
+  else
+    return false;
+}
+// arrowhead test: no contact shared by two trees other than the belt (tree 0); uniform, a scalar branch
+template <typename T, typename DIM>
+__device__ __forceinline__ bool arrow_substep(const Model<T>& M, const Ws<T, DIM>& w) {
+  if (M.dbg_flags & 16) return false;
+  uint64_t any = 0, both = 0;
+#pragma unroll
+  for (int t = 1; t < DIM::ntree; t++) {
+    const uint64_t m = w.tmask()[t];
+    const uint64_t mt = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
+    both |= any & mt;
+    any |= mt;
+  }
+  return both == 0;
+}
 
 template <typename T, typename DIM>
 __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
                                                T* dir) {
   constexpr int NV = DIM::nv, KK = DIM::K, AA = DIM::A, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
-  if (!(M.dbg_flags & 16)) {
-    // arrowhead test: no contact shared by two trees other than the belt (tree 0); uniform, a scalar branch
-    uint64_t any = 0, both = 0;
-#pragma unroll
-    for (int t = 1; t < NT; t++) {
-      const uint64_t m = w.tmask()[t];
-      const uint64_t mt = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
-      both |= any & mt;
-      any |= mt;
-    }
-    if (both == 0) {
-      chol_arrow_rl<T, DIM>(H, g, dir);
-      return;
-    }
+  if (arrow_substep(M, w)) {
+    chol_arrow_rl<T, DIM, false>(M, w, H, g, dir, 0);
+    return;
   }
   const int j = LANE;
   const int jo = j == NV - 1 ? 0 : j + 1;  // lane j's dof (original numbering)
@@ -2523,8 +2791,14 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
 //    forward-substitution row are accumulated afterwards in pivot order by a v_readlane chain.
 // Every entry sees the operations of chol_sparse_rl in the same order (the updates it skips are products with
 // exact zeros), so the factor and the direction are bit-identical to it.
-template <typename T, typename DIM>
-__device__ __forceinline__ void chol_arrow_rl(const T* H, const double* g, T* dir) {
+// ASM = true: H is not read from LDS but assembled straight into these registers (newton() skips the LDS
+// assembly on arrowhead substeps): lane j sums its column's M entries, the contacts of its own tree (K_c from
+// contact_K in CR_K: B_t' K_c B_t on its block rows, B_belt' K_c B_t on its belt row when the partner is the
+// belt) and the generic rows of its dof; the belt lane sums its diagonal over the belt's contacts.  Same terms
+// as the LDS assembly, summed per lane in contact order instead of by atomics (not bit-identical to it).
+template <typename T, typename DIM, bool ASM>
+__device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
+                                              T* dir, int nrow) {
   constexpr int NV = DIM::nv, A0 = 1 + 6 * DIM::K, NB = NV - 1;
   static_assert(NV <= WAVE, "one lane per position");
   const int j = LANE;
@@ -2533,12 +2807,81 @@ __device__ __forceinline__ void chol_arrow_rl(const T* H, const double* g, T* di
   const int ps = j < A0 - 1 ? (j / 6) * 6 : A0 - 1 + ((j - (A0 - 1)) / 9) * 9;  // own block's first position
   const int pn = j < A0 - 1 ? 6 : 9;         // own block's size
   const int jl = j - ps;                     // local index
-  T loc[9];
+  T loc[9], bel = T(0), hbb;
+  if constexpr (!ASM) {
 #pragma unroll
-  for (int ii = 0; ii < 9; ii++) loc[ii] = (blk && ii < pn) ? H[(ps + ii + 1) * NV + jo] : T(0);
-  T bel = blk ? H[jo] : T(0);  // row 0 (the belt) of column jo
-  const T hbb = H[0];
-  SYNC();
+    for (int ii = 0; ii < 9; ii++) loc[ii] = (blk && ii < pn) ? H[(ps + ii + 1) * NV + jo] : T(0);
+    bel = blk ? H[jo] : T(0);  // row 0 (the belt) of column jo
+    hbb = H[0];
+    SYNC();
+  } else {
+    // the belt lane assembles its diagonal as a block of one (tree 0, local index 0)
+    const bool bl = j == NV - 1;
+    const int t = bl ? 0 : (j < A0 - 1 ? 1 + j / 6 : 1 + DIM::K + (j - (A0 - 1)) / 9);
+    const int an = bl ? 1 : pn, al = bl ? 0 : jl;
+    if (blk && j >= A0 - 1) {
+      const T* Ma = w.Marm() + 81 * ((j - (A0 - 1)) / 9) + jl;
+#pragma unroll
+      for (int ii = 0; ii < 9; ii++) loc[ii] = Ma[9 * ii];
+    } else {
+      const T md = (blk || bl) ? Mdiag(M, w, jo) : T(0);
+#pragma unroll
+      for (int ii = 0; ii < 9; ii++) loc[ii] = ii == al ? md : T(0);
+    }
+    if (blk || bl) {
+      uint64_t mk = w.tmask()[t];
+      while (mk) {
+        const int c = __ffsll((unsigned long long)mk) - 1;
+        mk &= mk - 1;
+        const int* ci = w.ci() + 4 * c;
+        const T* cr = w.cr() + CR_N * c;
+        const T* Kc = cr + CR_K;
+        const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15;
+        const bool first = ta == t;
+        const int off = first ? 0 : nda;        // own tree's first column in the record
+        const int ob = first ? nda : 0;         // the partner's first column
+        const T* J = cr + CR_J;
+        const T k0 = Kc[0], k1 = Kc[1], k2 = Kc[2], k3 = Kc[3], k4 = Kc[4], k5 = Kc[5];
+        const T b0 = J[off + al], b1 = J[CJ + off + al], b2 = J[2 * CJ + off + al];
+        const T q0 = k0 * b0 + k3 * b1 + k4 * b2;
+        const T q1 = k3 * b0 + k1 * b1 + k5 * b2;
+        const T q2 = k4 * b0 + k5 * b1 + k2 * b2;
+        T jr0[9], jr1[9], jr2[9];
+#pragma unroll
+        for (int ii = 0; ii < 9; ii++) {
+          jr0[ii] = J[off + ii];
+          jr1[ii] = J[CJ + off + ii];
+          jr2[ii] = J[2 * CJ + off + ii];
+        }
+#pragma unroll
+        for (int ii = 0; ii < 9; ii++)
+          if (ii < an) loc[ii] += q0 * jr0[ii] + q1 * jr1[ii] + q2 * jr2[ii];
+        if ((first ? tb : ta) == 0) bel += q0 * J[ob] + q1 * J[CJ + ob] + q2 * J[2 * CJ + ob];
+      }
+      // generic rows (gripper equality, joint limits: both dofs in one arm) touching this dof
+      for (int r = 0; r < nrow; r++) {
+        const int* ri = w.ri() + 4 * r;
+        const T* rr = w.rr() + RR_N * r;
+        const int d0 = ri[0], d1 = ri[1];
+        if (d0 != jo && d1 != jo) continue;
+        if (!(ri[2] == 0 || *dslot(rr, RR_JAR) < 0.0)) continue;
+        const T D = rr[RR_D], c0 = rr[RR_C0], c1 = rr[RR_C1];
+        const T cj = d0 == jo ? c0 : c1;
+#pragma unroll
+        for (int ii = 0; ii < 9; ii++) {
+          const int d = ps + ii + 1;
+          if (d == d0) loc[ii] += D * c0 * cj;
+          if (d1 >= 0 && d == d1) loc[ii] += D * c1 * cj;
+        }
+      }
+    }
+    hbb = readlane(loc[0], NV - 1);
+    if (!blk) {
+#pragma unroll
+      for (int ii = 0; ii < 9; ii++) loc[ii] = T(0);
+    }
+    PMARK(PH_NHESS);
+  }
   const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
   T dinv = T(1), lbelt = T(0);
   static_for<0, 9>([&](auto sc) {
@@ -3341,6 +3684,40 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& 
   }
 }
 
+// gather_JtF by scatter ((2,4) scene): one lane per (contact, Jacobian column) adds its column's product with the
+// contact's frame force into a float64 accumulator by LDS atomics (one wave: a fixed order), one lane per generic
+// row likewise; the per-dof loop above is a chain of dependent LDS reads on the belt's lane, which carries every
+// belt contact.  acc: nv doubles of scratch (the solver's tmp, dead at the gradient and at the final forces).
+template <typename T, typename DIM, typename O>
+__device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, O* out,
+                                              double* acc) {
+  const DIM dm(M.dm);
+  for (int i = LANE; i < dm.nv; i += WAVE) acc[i] = 0.0;
+  SYNC();
+  for (int e = LANE; e < CJ * ncon; e += WAVE) {
+    const int c = e / CJ, ii = e - CJ * c;
+    const int* ci = w.ci() + 4 * c;
+    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+    const T* cr = w.cr() + CR_N * c;
+    const T* J = cr + CR_J;
+    const double* f3 = dslot(cr, CR_F3);
+    const double v = (double)J[ii] * f3[0] + (double)J[CJ + ii] * f3[1] + (double)J[2 * CJ + ii] * f3[2];
+    const int gi = ii < nda ? tree_dof(dm, ta) + ii : tree_dof(dm, tb >= 0 ? tb : 0) + ii - nda;
+    if (ii < nda + ndb) atomicAdd(acc + gi, v);
+  }
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    const T* rr = w.rr() + RR_N * r;
+    const double jar = *dslot(rr, RR_JAR);
+    if (!(ri[2] == 0 || jar < 0.0)) continue;
+    const double fr = (double)rr[RR_D] * jar;
+    atomicAdd(acc + ri[0], (double)rr[RR_C0] * fr);
+    if (ri[1] >= 0) atomicAdd(acc + ri[1], (double)rr[RR_C1] * fr);
+  }
+  SYNC();
+  for (int i = LANE; i < dm.nv; i += WAVE) out[i] = (O)acc[i];
+}
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
   const DIM dm(M.dm);
@@ -3384,12 +3761,16 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   PMARK(PH_NSETUP);
   int it;
   const int maxit = M.solver_iter;
+  const bool scatter = arrow_scene<T, DIM>() && !(M.dbg_flags & 64);  // gather_JtF_sc (FM_NO_SCATTER=1: off)
   const int ntri = nv * (nv + 1) / 2;
   for (it = 0; it < maxit; it++) {
     // gradient g = M(a - as) + J' D jar (active)
     contact_f3(w, ncon);
     SYNC();
-    gather_JtF(M, w, ncon, nrow, g, false);
+    if (scatter)
+      gather_JtF_sc(M, w, ncon, nrow, g, tmp);
+    else
+      gather_JtF(M, w, ncon, nrow, g, false);
     SYNC();
     double gn = 0;
     for (int i = LANE; i < nv; i += WAVE) {
@@ -3399,6 +3780,19 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     gn = wave_sum(gn);
     PMARK(PH_NGRAD);
     if (scale * sqrt(gn) < tol) break;
+    // arrowhead substeps of the (2,4) scene (no contact couples two trees other than the belt: nearly every
+    // substep): H is assembled straight into the block-parallel factor's registers, no LDS Hessian
+    bool solved = false;
+    if constexpr (arrow_scene<T, DIM>()) {
+      if (!(M.dbg_flags & 32) && arrow_substep(M, w)) {
+        contact_K(w, ncon);
+        SYNC();
+        chol_arrow_rl<T, DIM, true>(M, w, H, g, dir, nrow);
+        PMARK(PH_NCHOL);
+        solved = true;
+      }
+    }
+    if (!solved) {
     // Hessian H = M + sum_c B_c' K_c B_c + generic rows
     {
       // zero fill in 16-byte stores (the region is 16-byte aligned), then the tail
@@ -3534,6 +3928,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
         SYNC();
       }
     }
+    }  // !solved
     PMARK(PH_NSOLVE);
     // exact line search along dir (segment walking over the breakpoints of the inequality rows)
     // Jd per contact (frame components) and per generic row
@@ -3671,7 +4066,10 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   // final constraint forces at a
   contact_f3(w, ncon);
   SYNC();
-  gather_JtF(M, w, ncon, nrow, w.fc(), false);
+  if (scatter)
+    gather_JtF_sc(M, w, ncon, nrow, w.fc(), tmp);
+  else
+    gather_JtF(M, w, ncon, nrow, w.fc(), false);
   SYNC();
   for (int i = LANE; i < nv; i += WAVE) w.fc()[i] = -w.fc()[i];
   for (int r = LANE; r < nrow; r += WAVE) {

@@ -1,6 +1,7 @@
 """Bit-identity and timing of the arrowhead Cholesky fast path (chol_arrow_rl) against the general register
-Cholesky (FM_NO_ARROW=1) on the (2,4) scene: the same states stepped with the same actions under both switches,
-full state records compared bitwise.  usage: python tools/arrow_probe.py [--arenas N] [--steps K]"""
+Cholesky (FM_NO_ARROW=1) on the (2,4) scene: the same states stepped with the same actions under each switch,
+full state records compared bitwise.  The arrowhead factor of the LDS-assembled Hessian (FM_NO_ARROW=2) is
+bit-identical to the general one; the default (Hessian assembled in registers) sums in another order.  usage: python tools/arrow_probe.py [--arenas N] [--steps K]"""
 import argparse
 import json
 import os
@@ -15,11 +16,13 @@ from factory_marl_amd import FactoryVecEnv  # noqa: E402
 from factory_marl_amd.environments import run_kwargs  # noqa: E402
 
 
-def run(env, s0, acts, arrow):
-    if arrow:
-        os.environ.pop("FM_NO_ARROW", None)
+def run(env, s0, acts, mode):
+    """mode "" = default (Hessian assembled in the arrowhead factor's registers), "1" = general register Cholesky,
+    "2" = arrowhead factor of the LDS-assembled Hessian"""
+    if mode:
+        os.environ["FM_NO_ARROW"] = mode
     else:
-        os.environ["FM_NO_ARROW"] = "1"
+        os.environ.pop("FM_NO_ARROW", None)
     env.set_state(s0)
     env.sync()
     t0 = time.perf_counter()
@@ -49,14 +52,17 @@ def main():
         env.sync()
         s0 = env.get_state()
         acts = [torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1 for _ in range(args.steps)]
-        run(env, s0, acts[:3], True)  # warm
-        sa, ta = run(env, s0, acts, True)
-        sg, tg = run(env, s0, acts, False)
-        sa2, ta2 = run(env, s0, acts, True)
-        diff = int((sa != sg).any(axis=1).sum())
-        rep = int((sa != sa2).any(axis=1).sum())
-        out[prec] = dict(arenas=n, steps=args.steps, arenas_differing=diff, rerun_differing=rep,
-                         ms_per_step_arrow=1e3 * min(ta, ta2) / args.steps, ms_per_step_general=1e3 * tg / args.steps)
+        run(env, s0, acts[:3], "")  # warm
+        sa, ta = run(env, s0, acts, "")
+        sg, tg = run(env, s0, acts, "1")
+        sl, tl = run(env, s0, acts, "2")
+        sa2, ta2 = run(env, s0, acts, "")
+        out[prec] = dict(arenas=n, steps=args.steps,
+                         lds_arrow_vs_general_differing=int((sl != sg).any(axis=1).sum()),
+                         reg_asm_vs_general_differing=int((sa != sg).any(axis=1).sum()),
+                         rerun_differing=int((sa != sa2).any(axis=1).sum()),
+                         ms_per_step_reg_asm=1e3 * min(ta, ta2) / args.steps, ms_per_step_lds_arrow=1e3 * tl / args.steps,
+                         ms_per_step_general=1e3 * tg / args.steps)
         print(prec, out[prec], flush=True)
         env.close()
     os.environ.pop("FM_NO_ARROW", None)
