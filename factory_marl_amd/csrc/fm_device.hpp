@@ -2652,7 +2652,7 @@ __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_
 //    substep -- H in this order is block diagonal with a belt border, and the tree blocks factor independently.
 template <typename T, typename DIM, bool ASM>
 __device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
-                                              T* dir, int nrow);
+                                              T* dir, int ncon, int nrow);
 
 // scenes with the register Cholesky on one 64-contact tree-mask word ((2,4), fp32 and fp64)
 template <typename T, typename DIM>
@@ -2682,7 +2682,7 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
                                                T* dir) {
   constexpr int NV = DIM::nv, KK = DIM::K, AA = DIM::A, NT = DIM::ntree, A0 = 1 + 6 * DIM::K;
   if (arrow_substep(M, w)) {
-    chol_arrow_rl<T, DIM, false>(M, w, H, g, dir, 0);
+    chol_arrow_rl<T, DIM, false>(M, w, H, g, dir, 0, 0);
     return;
   }
   const int j = LANE;
@@ -2798,7 +2798,7 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
 // as the LDS assembly, summed per lane in contact order instead of by atomics (not bit-identical to it).
 template <typename T, typename DIM, bool ASM>
 __device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM>& w, const T* H, const double* g,
-                                              T* dir, int nrow) {
+                                              T* dir, int ncon, int nrow) {
   constexpr int NV = DIM::nv, A0 = 1 + 6 * DIM::K, NB = NV - 1;
   static_assert(NV <= WAVE, "one lane per position");
   const int j = LANE;
@@ -2828,7 +2828,26 @@ __device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM
 #pragma unroll
       for (int ii = 0; ii < 9; ii++) loc[ii] = ii == al ? md : T(0);
     }
-    if (blk || bl) {
+    // the belt's diagonal: one lane per contact (B_belt' K_c B_belt of the contacts on the belt), then a wave sum
+    // -- the belt lane would otherwise walk every belt contact while a cube lane walks four
+    {
+      T hb = T(0);
+      if (j < ncon) {
+        const int* ci = w.ci() + 4 * j;
+        const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15;
+        if (ta == 0 || tb == 0) {
+          const T* cr = w.cr() + CR_N * j;
+          const T* Kc = cr + CR_K;
+          const int cb = ta == 0 ? 0 : nda;
+          const T b0 = cr[CR_J + cb], b1 = cr[CR_J + CJ + cb], b2 = cr[CR_J + 2 * CJ + cb];
+          hb = b0 * (Kc[0] * b0 + Kc[3] * b1 + Kc[4] * b2) + b1 * (Kc[3] * b0 + Kc[1] * b1 + Kc[5] * b2) +
+               b2 * (Kc[4] * b0 + Kc[5] * b1 + Kc[2] * b2);
+        }
+      }
+      hb = wave_sum(hb);
+      if (bl) loc[0] += hb;
+    }
+    if (blk) {
       uint64_t mk = w.tmask()[t];
       while (mk) {
         const int c = __ffsll((unsigned long long)mk) - 1;
@@ -3787,7 +3806,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       if (!(M.dbg_flags & 32) && arrow_substep(M, w)) {
         contact_K(w, ncon);
         SYNC();
-        chol_arrow_rl<T, DIM, true>(M, w, H, g, dir, nrow);
+        chol_arrow_rl<T, DIM, true>(M, w, H, g, dir, ncon, nrow);
         PMARK(PH_NCHOL);
         solved = true;
       }
