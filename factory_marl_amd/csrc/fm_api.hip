@@ -191,6 +191,8 @@ static Model<T> make_model(const fm_handle* h) {
   if (ns && ns[0] == '1') M.dbg_flags |= 64;
   const char* sf = getenv("FM_SERIAL_FK");  // experiment switch: arm kinematics / RNE on one lane per arm
   if (sf && sf[0] == '1') M.dbg_flags |= 128;
+  const char* fs = getenv("FM_TWO_PASS_SETUP");  // experiment switch: the warmstart candidates in two row passes
+  if (fs && fs[0] == '1') M.dbg_flags |= 256;
   return M;
 }
 

@@ -125,7 +125,8 @@ struct Model {
                              // (FM_NO_MIDCACHE=1); bit 4 = no arrowhead Cholesky (FM_NO_ARROW=1); bit 5 = the
                              // arrowhead factor of the LDS-assembled Hessian (FM_NO_ARROW=2); bit 6 = the per-dof
                              // gather of J' f instead of the scatter (FM_NO_SCATTER=1); bit 7 = the serial arm
-                             // kinematics (FM_SERIAL_FK=1)
+                             // kinematics (FM_SERIAL_FK=1); bit 8 = the Newton warmstart's two row passes
+                             // (FM_TWO_PASS_SETUP=1)
 };
 
 template <typename T>

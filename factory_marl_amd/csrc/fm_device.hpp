@@ -511,9 +511,17 @@ template <typename T, typename DIM>
 __device__ constexpr bool dense_mfma_chol();
 // narrowphase split of the compile-time scenes without the dense Cholesky (whose sub-phase slots it borrows):
 // PH_CHDIAG = geom-pair expansion, PH_CHPANEL = sphere / plane pairs, PH_CHTRAIL = box-box pairs
-#define NPMARK(k)                                                       \
-  do {                                                                  \
-    if constexpr (DIM::fixed && !dense_mfma_chol<T, DIM>()) PMARK(k);   \
+#ifndef FM_PROF_SPLIT
+#define FM_PROF_SPLIT 0  // experiment builds only: 1 / 2 lend the narrowphase slots to sub-phases of rows + setup /
+                         // gradient + line search (SPLITMARK below)
+#endif
+#define NPMARK(k)                                                                         \
+  do {                                                                                    \
+    if constexpr (FM_PROF_SPLIT == 0 && DIM::fixed && !dense_mfma_chol<T, DIM>()) PMARK(k); \
+  } while (0)
+#define SPLITMARK(v, k)                                                               \
+  do {                                                                                \
+    if constexpr (FM_PROF_SPLIT == (v) && DIM::fixed && !dense_mfma_chol<T, DIM>()) PMARK(k); \
   } while (0)
 
 // ------------------------------------------------------------------------------------------------
@@ -2425,8 +2433,10 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     cr[CR_BD] = (T)Bb;
   }
   SYNC();
+  SPLITMARK(1, PH_CHDIAG);
   // efc velocity in the contact frame
   contact_jx<T>(M, w, v, ncon, CR_VEL);
+  SPLITMARK(1, PH_CHPANEL);
   // ---- generic rows: gripper joint equality + active joint limits.  One candidate row per lane in the
   // reference's order (per arm: the equality, then each dof's lower and upper limit), compacted by ballot
   {
@@ -2487,6 +2497,7 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     if (LANE == 0) misc[MISC_NROW] = nr < dm.maxrow ? nr : dm.maxrow;
   }
   SYNC();
+  SPLITMARK(1, PH_CHTRAIL);
   // ---- tree -> contact masks: one ballot per tree and 64-contact word (word h holds contacts 64 h .. 64 h + 63)
   {
     const int nh = DIM::MAXC == WAVE ? 1 : (dm.maxcon + WAVE - 1) / WAVE;
@@ -2666,13 +2677,17 @@ __device__ constexpr bool arrow_scene() {
 template <typename T, typename DIM>
 __device__ __forceinline__ bool arrow_substep(const Model<T>& M, const Ws<T, DIM>& w) {
   if (M.dbg_flags & 16) return false;
-  uint64_t any = 0, both = 0;
+  uint64_t both = 0;
 #pragma unroll
-  for (int t = 1; t < DIM::ntree; t++) {
-    const uint64_t m = w.tmask()[t];
-    const uint64_t mt = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
-    both |= any & mt;
-    any |= mt;
+  for (int h = 0; h < DIM::MAXC / WAVE; h++) {  // tree-mask words (contacts 64 h .. 64 h + 63)
+    uint64_t any = 0;
+#pragma unroll
+    for (int t = 1; t < DIM::ntree; t++) {
+      const uint64_t m = w.tmask()[h * DIM::ntree + t];
+      const uint64_t mt = ((uint64_t)(unsigned)rfl((int)(m >> 32)) << 32) | (unsigned)rfl((int)(m & 0xffffffffu));
+      both |= any & mt;
+      any |= mt;
+    }
   }
   return both == 0;
 }
@@ -2964,6 +2979,125 @@ __device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM
   });
   if (blk) dir[jo] = x;
   if (j == NV - 1) dir[0] = xb;
+  SYNC();
+}
+
+// Arrowhead Cholesky of the bordered scenes ((2,8), (2,10): 64 < nv <= 80, LDS-assembled Hessian): the block
+// positions do not fit one lane each, so chol_arrow_rl's block steps run in two passes of whole blocks -- positions
+// [0, SPLIT) on lanes 0.., [SPLIT, nv - 1) on lanes 0.. again (SPLIT = the last block boundary <= 64) -- with one
+// register set per pass; the belt's diagonal and forward row are v_readlane chains over both passes in pivot
+// order.  Used when no contact couples two trees other than the belt, instead of the bordered register factor.
+template <typename T, typename DIM>
+__device__ constexpr int arrow_split() {
+  constexpr int A0 = 1 + 6 * DIM::K;
+  int sp = 0;
+  for (int c = 0; c <= DIM::K; c++)
+    if (6 * c <= WAVE) sp = 6 * c;
+  for (int a = 0; a <= DIM::A; a++)
+    if (A0 - 1 + 9 * a <= WAVE) sp = A0 - 1 + 9 * a;
+  return sp;
+}
+template <typename T, typename DIM>
+__device__ __forceinline__ void chol_arrow2_rl(const T* H, const double* g, T* dir) {
+  constexpr int NV = DIM::nv, A0 = 1 + 6 * DIM::K, NB = NV - 1, SPLIT = arrow_split<T, DIM>();
+  static_assert(SPLIT <= WAVE && NB - SPLIT <= WAVE && NB > WAVE, "two passes of whole blocks");
+  const int j = LANE;
+  bool blk[2];
+  int ps[2], pn[2], jl[2], jo[2];
+  T loc[2][9], bel[2], dinv[2], lbelt[2];
+#pragma unroll
+  for (int P = 0; P < 2; P++) {
+    const int base = P ? SPLIT : 0, end = P ? NB : SPLIT;
+    const int p = base + j;
+    blk[P] = p < end;
+    const int pa = p < A0 - 1 ? (p / 6) * 6 : A0 - 1 + ((p - (A0 - 1)) / 9) * 9;  // block start (position)
+    pn[P] = p < A0 - 1 ? 6 : 9;
+    jl[P] = p - pa;
+    ps[P] = pa - base;  // block start (lane)
+    jo[P] = p + 1;
+#pragma unroll
+    for (int ii = 0; ii < 9; ii++) loc[P][ii] = (blk[P] && ii < pn[P]) ? H[(pa + ii + 1) * NV + jo[P]] : T(0);
+    bel[P] = blk[P] ? H[jo[P]] : T(0);
+    dinv[P] = T(1);
+    lbelt[P] = T(0);
+  }
+  const T hbb = H[0];
+  SYNC();
+  const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-37);
+#pragma unroll
+  for (int P = 0; P < 2; P++) {
+    static_for<0, 9>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const bool act = blk[P] && s < pn[P];
+      const int p = (ps[P] + s) & (WAVE - 1);
+      T d = __shfl(loc[P][s], p);
+      d = d > tiny ? d : tiny;
+      const T ri = T(1) / sqrt(d);
+      const T lj = loc[P][s] * ri;
+      const T lb = __shfl(bel[P], p) * ri;
+      if (act && jl[P] == s) {
+        dinv[P] = ri;
+        lbelt[P] = lb;
+      }
+      if (act && jl[P] >= s) loc[P][s] = lj;
+      T lv[9];
+#pragma unroll
+      for (int ii = s + 1; ii < 9; ii++) lv[ii] = __shfl(lj, (ps[P] + ii) & (WAVE - 1));
+      if (act && jl[P] > s) {
+#pragma unroll
+        for (int ii = s + 1; ii < 9; ii++)
+          if (ii < pn[P]) loc[P][ii] -= lv[ii] * lj;
+        bel[P] -= lb * lj;
+      }
+    });
+  }
+  T db = hbb;
+#pragma unroll
+  for (int k = 0; k < SPLIT; k++) {
+    const T x = readlane(lbelt[0], k);
+    db -= x * x;
+  }
+#pragma unroll
+  for (int k = 0; k < NB - SPLIT; k++) {
+    const T x = readlane(lbelt[1], k);
+    db -= x * x;
+  }
+  db = db > tiny ? db : tiny;
+  const T rib = T(1) / sqrt(db);
+  T y[2];
+  T accb = (T)-g[0];
+#pragma unroll
+  for (int P = 0; P < 2; P++) {
+    T acc = blk[P] ? (T)-g[jo[P]] : T(0);
+    y[P] = T(0);
+    static_for<0, 9>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const bool act = blk[P] && s < pn[P];
+      const T yk = __shfl(acc * dinv[P], (ps[P] + s) & (WAVE - 1));
+      if (act && jl[P] == s) y[P] = yk;
+      if (act && jl[P] > s) acc -= loc[P][s] * yk;
+    });
+  }
+#pragma unroll
+  for (int k = 0; k < SPLIT; k++) accb -= readlane(lbelt[0], k) * readlane(y[0], k);
+#pragma unroll
+  for (int k = 0; k < NB - SPLIT; k++) accb -= readlane(lbelt[1], k) * readlane(y[1], k);
+  const T xb = (accb * rib) * rib;
+#pragma unroll
+  for (int P = 0; P < 2; P++) {
+    T acc2 = y[P];
+    if (blk[P]) acc2 -= bel[P] * dinv[P] * xb;
+    T x = T(0);
+    static_for<0, 9>([&](auto sc) {
+      constexpr int s = 8 - decltype(sc)::value;
+      const bool act = blk[P] && s < pn[P];
+      const T xk = __shfl(acc2 * dinv[P], (ps[P] + s) & (WAVE - 1));
+      if (act && jl[P] == s) x = xk;
+      if (act && jl[P] < s) acc2 -= loc[P][s] * dinv[P] * xk;
+    });
+    if (blk[P]) dir[jo[P]] = x;
+  }
+  if (j == 0) dir[0] = xb;
   SYNC();
 }
 
@@ -3596,12 +3730,13 @@ __device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& 
 
 // constraint part of the primal cost at the current CR_JA / RR_JAR: sum of 1/2 D jar^2 over active rows
 template <typename T, typename DIM>
-__device__ __forceinline__ double rows_cost(const Ws<T, DIM>& w, int ncon, int nrow) {
+__device__ __forceinline__ double rows_cost(const Ws<T, DIM>& w, int ncon, int nrow, int cslot = CR_JA,
+                                            int rslot = RR_JAR) {
   double cst = 0;
   for (int c = LANE; c < ncon; c += WAVE) {
     const T* cr = w.cr() + CR_N * c;
     const T mu = cr[CR_MU], D = cr[CR_D], bd = cr[CR_BD], kd = cr[CR_KD];
-    const double* ja = dslot(cr, CR_JA);
+    const double* ja = dslot(cr, cslot);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       const T aref = -bd * edge_val(cr + CR_VEL, mu, e) - kd;
@@ -3612,10 +3747,51 @@ __device__ __forceinline__ double rows_cost(const Ws<T, DIM>& w, int ncon, int n
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
     const T* rr = w.rr() + RR_N * r;
-    const double jar = *dslot(rr, RR_JAR);
+    const double jar = *dslot(rr, rslot);
     if (ri[2] == 0 || jar < 0.0) cst += 0.5 * (double)rr[RR_D] * jar * jar;
   }
   return wave_sum(cst);
+}
+
+// Newton warmstart (newton()): both candidates' row products in one pass -- B qacc_smooth into the line search's
+// JD slots (free until then), B qacc_warmstart into JA; generic rows likewise (RR_JD / RR_JAR, minus aref).  The
+// same products rows_eval forms, one J load for both.
+template <typename T, typename DIM>
+__device__ __forceinline__ void rows_eval2(const Model<T>& M, const Ws<T, DIM>& w, const T* xs, const double* xw,
+                                           int ncon, int nrow) {
+  const DIM dm(M.dm);
+  for (int e = LANE; e < 3 * ncon; e += WAVE) {
+    const int c = e / 3, r = e - 3 * c;
+    const int* ci = w.ci() + 4 * c;
+    T* cr = w.cr() + CR_N * c;
+    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+    const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+    const T* J = cr + CR_J + r * CJ;
+    const T* Jb = J + nda;
+    double s1 = 0, s2 = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const double ja = j < nda ? (double)J[j] : 0.0;
+      s1 += ja * (double)xs[oa + j];
+      s2 += ja * xw[oa + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const double jb = j < ndb ? (double)Jb[j] : 0.0;
+      s1 += jb * (double)xs[ob + j];
+      s2 += jb * xw[ob + j];
+    }
+    dslot(cr, CR_JD)[r] = s1;
+    dslot(cr, CR_JA)[r] = s2;
+  }
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    T* rr = w.rr() + RR_N * r;
+    *dslot(rr, RR_JD) = (double)rr[RR_C0] * (double)xs[ri[0]] +
+                        (ri[1] >= 0 ? (double)rr[RR_C1] * (double)xs[ri[1]] : 0.0) - (double)rr[RR_AREF];
+    *dslot(rr, RR_JAR) = (double)rr[RR_C0] * xw[ri[0]] + (ri[1] >= 0 ? (double)rr[RR_C1] * xw[ri[1]] : 0.0) -
+                         (double)rr[RR_AREF];
+  }
 }
 
 // evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
@@ -3765,17 +3941,47 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   // warmstart: the cheaper of qacc_warmstart and qacc_smooth.  The smooth candidate is evaluated first (its
   // quadratic part is zero), so in the common case (the warmstart wins) the row products and M(a - as) left
   // behind are already those of the chosen start and need no third evaluation
-  const double c_sm = rows_eval(M, w, as, ncon, nrow);
-  SYNC();
-  double qc = quad(a);
-  double cost = qc + rows_eval(M, w, a, ncon, nrow);
-  SYNC();
-  if (!(cost < c_sm)) {
-    for (int i = LANE; i < nv; i += WAVE) a[i] = (double)as[i];
+  double qc, cost;
+  if (!(M.dbg_flags & 256)) {
+    // both candidates' row products in one pass (rows_eval2); the smooth candidate's land in the JD slots
+    rows_eval2(M, w, as, a, ncon, nrow);
     SYNC();
+    const double c_sm = rows_cost(w, ncon, nrow, CR_JD, RR_JD);
+    const double c_ws = rows_cost(w, ncon, nrow);
+    SPLITMARK(1, PH_CHSOLVE);
+    qc = quad(a);
+    cost = qc + c_ws;
+    SYNC();
+    if (!(cost < c_sm)) {
+      // the smooth candidate wins: a = qacc_smooth, its products move into JA (its quadratic part is zero)
+      for (int i = LANE; i < nv; i += WAVE) a[i] = (double)as[i];
+      for (int e = LANE; e < 3 * ncon; e += WAVE) {
+        T* cr = w.cr() + CR_N * (e / 3);
+        dslot(cr, CR_JA)[e % 3] = dslot(cr, CR_JD)[e % 3];
+      }
+      for (int r = LANE; r < nrow; r += WAVE) {
+        T* rr = w.rr() + RR_N * r;
+        *dslot(rr, RR_JAR) = *dslot(rr, RR_JD);
+      }
+      SYNC();
+      qc = quad(a);
+      cost = qc + c_sm;
+      SYNC();
+    }
+  } else {
+    const double c_sm = rows_eval(M, w, as, ncon, nrow);
+    SYNC();
+    SPLITMARK(1, PH_CHSOLVE);
     qc = quad(a);
     cost = qc + rows_eval(M, w, a, ncon, nrow);
     SYNC();
+    if (!(cost < c_sm)) {
+      for (int i = LANE; i < nv; i += WAVE) a[i] = (double)as[i];
+      SYNC();
+      qc = quad(a);
+      cost = qc + rows_eval(M, w, a, ncon, nrow);
+      SYNC();
+    }
   }
   PMARK(PH_NSETUP);
   int it;
@@ -3786,11 +3992,13 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     // gradient g = M(a - as) + J' D jar (active)
     contact_f3(w, ncon);
     SYNC();
+    SPLITMARK(2, PH_CHDIAG);
     if (scatter)
       gather_JtF_sc(M, w, ncon, nrow, g, tmp);
     else
       gather_JtF(M, w, ncon, nrow, g, false);
     SYNC();
+    SPLITMARK(2, PH_CHPANEL);
     double gn = 0;
     for (int i = LANE; i < nv; i += WAVE) {
       g[i] += Ma[i];
@@ -3901,7 +4109,12 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       chol_solve_reg<T, 64>(H, w.bc(), nv, g, dir);
       PMARK(PH_NCHOL);
     } else if (border_chol<T, DIM>() && !(M.dbg_flags & 1)) {
-      if constexpr (border_chol<T, DIM>()) chol_sparse_border<DIM>(M, w, H, g, dir);
+      if constexpr (border_chol<T, DIM>()) {
+        if (arrow_substep(M, w))
+          chol_arrow2_rl<T, DIM>(H, g, dir);
+        else
+          chol_sparse_border<DIM>(M, w, H, g, dir);
+      }
       PMARK(PH_NCHOL);
     } else if (dense_mfma_chol<T, DIM>() && nv > 80 && !(M.dbg_flags & 3)) {  // hstride() pads these
       if constexpr (dense_mfma_chol<T, DIM>()) chol_dense_mfma<DIM>(M, w, H, nv, g, dir);
@@ -3967,6 +4180,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     }
     dMd = wave_sum(dMd);
     dMa = wave_sum(dMa);
+    SPLITMARK(2, PH_CHTRAIL);
     // the walk's per-row data is loop-invariant: the contacts (4 pyramid edges each; contact LANE + 64 h) and
     // one generic row per lane (nrow <= 64) held in registers; padding slots carry jd = 0, D = 0 and contribute
     // nothing
@@ -4054,6 +4268,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       }
       alpha = tn;
     }
+    SPLITMARK(2, PH_CHSOLVE);
     // step: a, M (a - as) and the row products all move along dir (MuJoCo's Newton updates Jaref and Ma
     // the same way instead of recomputing them); the quadratic part of the cost follows exactly
     for (int i = LANE; i < nv; i += WAVE) {

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from factory_marl_amd import FactoryVecEnv  # noqa: E402
 from factory_marl_amd.environments import run_kwargs  # noqa: E402
 
-SWITCHES = ("FM_NO_ARROW", "FM_NO_SCATTER", "FM_SERIAL_FK", "FM_NO_MIDCACHE", "FM_SERIAL_BOXBOX", "FM_CHOL_LDS")
+SWITCHES = ("FM_NO_ARROW", "FM_NO_SCATTER", "FM_SERIAL_FK", "FM_TWO_PASS_SETUP", "FM_NO_MIDCACHE", "FM_SERIAL_BOXBOX", "FM_CHOL_LDS")
 
 
 def apply(setting):
