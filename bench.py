@@ -228,10 +228,30 @@ def free_port():
     return port
 
 
-def spawn_ranks(n, argv):
+WATCHDOG_RC = 3  # exit code of a job the watchdog stopped
+
+
+def stop_ranks(procs, grace=10.0):
+    """SIGTERM every live rank, SIGKILL whatever is still alive after `grace` seconds"""
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    t0 = time.monotonic()
+    while any(p.poll() is None for p in procs) and time.monotonic() - t0 < grace:
+        time.sleep(0.1)
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+
+
+def spawn_ranks(n, argv, deadline):
     """`bench.py --gpus N` without a torchrun environment: N rank processes of this script, one GPU each, 127.0.0.1
     rendezvous.  The parent never touches the GPU (it only waits), so nothing is exec'd from a GPU process; rank 0
-    prints the JSON line.  Returns the first non-zero rank exit code (the other ranks are then stopped)."""
+    prints the JSON line.  Returns the first non-zero rank exit code (the other ranks are then stopped).
+    Watchdog: a job still running `deadline` seconds after launch (a rank stuck in a collective holds every other
+    rank in it) is stopped -- every rank terminated, the ranks that had not finished named on stderr -- and the
+    parent exits with WATCHDOG_RC."""
     port = free_port()
     procs = []
     for r in range(n):
@@ -239,17 +259,23 @@ def spawn_ranks(n, argv):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
     rc = 0
-    pending = list(procs)
+    pending = list(range(n))
+    t0 = time.monotonic()
     while pending:
-        for p in list(pending):
-            code = p.poll()
+        for r in list(pending):
+            code = procs[r].poll()
             if code is None:
                 continue
-            pending.remove(p)
+            pending.remove(r)
             if code != 0 and rc == 0:
                 rc = code
-                for q in pending:
-                    q.terminate()
+                print(f"bench.py: rank {r} exited with {code}; stopping ranks {pending}", file=sys.stderr, flush=True)
+                stop_ranks([procs[q] for q in pending])
+        if pending and deadline > 0 and time.monotonic() - t0 > deadline:
+            print(json.dumps({"error": "watchdog", "deadline_s": deadline, "ranks_unfinished": pending,
+                              "ranks_finished": [r for r in range(n) if r not in pending]}), file=sys.stderr, flush=True)
+            stop_ranks([procs[q] for q in pending])
+            return WATCHDOG_RC
         time.sleep(0.2)
     return rc
 
@@ -259,7 +285,7 @@ def resolve_world(args):
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None:
         if args.gpus is not None and args.gpus > 1:
-            return spawn_ranks(args.gpus, sys.argv[1:])
+            return spawn_ranks(args.gpus, sys.argv[1:], args.deadline)
         args.gpus = 1
         return None
     w = int(env_world)
@@ -277,17 +303,20 @@ def main_dry_run(args):
 
     ctx = RankContext.from_env(use_gpu=False)
     lo, hi = rank_arenas(args.arenas, ctx.world, ctx.rank, args.scaling)
+    if args.stall_rank == ctx.rank:
+        time.sleep(args.stall_seconds)  # watchdog test: this rank arrives late at the collectives below
     ranges = [None] * ctx.world
     if ctx.distributed:
         dist.all_gather_object(ranges, (lo, hi))
     else:
         ranges = [(lo, hi)]
+    per_rank = ctx.gather_rank_times(1.0 + 0.5 * ctx.rank, 0.0)
     wall = ctx.max_over_ranks(1.0 + 0.5 * ctx.rank)
     total = ctx.sum_over_ranks(hi - lo)
     if ctx.rank == 0:
         print(json.dumps({"metric": "dry run (launcher only)", "n_gpus": ctx.world, "scaling": args.scaling,
                           "backend": ctx.backend, "rank_arenas": [list(r) for r in ranges], "total_arenas": int(total),
-                          "wall_max": wall, "value": total * args.steps / wall}), flush=True)
+                          "wall_max": wall, "value": total * args.steps / wall, "per_rank": per_rank}), flush=True)
     ctx.close()
 
 
@@ -324,6 +353,10 @@ def main():
                     help="config2: the headline (random policy); config3: 16384 arenas 2x8 PPO rollout; config4: "
                          "131072 arenas 2x8 PPO rollout strong-split over the ranks (RCCL update); config5: "
                          "4 arms x 16 objects PauseIKToggleEnv, 4096 arenas per GPU (32768 on 8), random toggles")
+    ap.add_argument("--deadline", type=float, default=1200.0,
+                    help="--gpus N launcher: stop every rank and exit non-zero after this many seconds (0 = none)")
+    ap.add_argument("--stall-rank", type=int, default=-1, help=argparse.SUPPRESS)  # watchdog test (--dry-run)
+    ap.add_argument("--stall-seconds", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--ppo-batch", type=int, default=16384)
     ap.add_argument("--ppo-epochs", type=int, default=10)
     args = ap.parse_args()
@@ -348,6 +381,7 @@ def main():
     N = hi - lo  # this rank's arenas
     NJ = job_arenas(args, ctx.world)
     wall, kern_ms, dc = timed_run(ctx, args, args.precision, args.steps, args.warmup, lo, hi)
+    per_rank = ctx.gather_rank_times(wall, kern_ms)
     wall = ctx.max_over_ranks(wall)
     value = NJ * args.steps / wall
     diag = diagnostics(dc, N, args.steps)
@@ -403,6 +437,8 @@ def main():
             "roofline": roof,
             "diagnostics": diag,
         }
+        if ctx.world > 1:
+            line["per_rank"] = per_rank
         if fp64 is not None:
             line["fp64_value"] = fp64
         if ctx.world == 1 and not args.no_cpu_baseline:
@@ -426,6 +462,7 @@ def main_config5(args):
     lo, hi = rank_arenas(args.arenas, ctx.world, ctx.rank, args.scaling)
     N = hi - lo
     wall, kern_ms, dc = timed_run(ctx, args, args.precision, args.steps, args.warmup, lo, hi)
+    per_rank = ctx.gather_rank_times(wall, kern_ms)
     wall = ctx.max_over_ranks(wall)
     value = job_arenas(args, ctx.world) * args.steps / wall
     if ctx.rank == 0:
@@ -443,6 +480,8 @@ def main_config5(args):
             "kernel_ms_avg": round(kern_ms, 4),
             "diagnostics": diagnostics(dc, N, args.steps),
         }
+        if ctx.world > 1:
+            line["per_rank"] = per_rank
         print(json.dumps(line), flush=True)
     ctx.close()
 
@@ -467,6 +506,7 @@ def main_config3(args):
     N = hi - lo
     NJ = job_arenas(args, ctx.world)
     wall, train_s, dc = timed_run_ppo(ctx, args, lo, hi)
+    per_rank = ctx.gather_rank_times(wall, train_s * 1e3)
     wall = ctx.max_over_ranks(wall)
     train_s = ctx.max_over_ranks(train_s)
     value = NJ * args.steps / wall
@@ -495,6 +535,8 @@ def main_config3(args):
             "iteration_env_steps_per_s": round(samples / (wall + train_s), 2),
             "diagnostics": diagnostics(dc, N, args.steps),
         }
+        if ctx.world > 1:
+            line["per_rank"] = per_rank  # kernel_ms = this rank's PPO update
         print(json.dumps(line), flush=True)
     ctx.close()
 

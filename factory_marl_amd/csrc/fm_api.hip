@@ -1,6 +1,8 @@
 // fm_api.hip -- host side of libfactorysim.so: scene upload, workspace layout, kernel dispatch and the
 // C ABI declared in include/factorysim.h.  The runtime-dims kernels are instantiated here; the
 // compile-time scene kernels live in fm_fixed.hip objects (one per scene in FM_FIXED_SCENES).
+#include <cstdio>
+
 #include "fm_device.hpp"
 #include "fm_render.hpp"
 
@@ -92,6 +94,7 @@ struct fm_handle {
   int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
   Lay lay_step{};  // workspace layout of the env-step kernel in use
   bool spill = false;          // DimsSpill: Hessian + contact records in per-arena global scratch (fp64, > 160 KiB)
+  uint32_t xflags = 0;         // experiment switches (Model::dbg_flags): read once at fm_create, fm_set_param
   char* spill_buf = nullptr;   // [N][lay.gtotal]
 };
 
@@ -178,22 +181,37 @@ static Model<T> make_model(const fm_handle* h) {
   M.meaninertia = (const T*)h->meaninertia;
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
-  const char* cl = getenv("FM_CHOL_LDS");
-  M.dbg_flags = (cl && cl[0] == '1') ? 1 : ((cl && cl[0] == '2') ? 2 : 0);
-  const char* sb = getenv("FM_SERIAL_BOXBOX");  // experiment switch: one lane per box-box pair throughout
-  if (sb && sb[0] == '1') M.dbg_flags |= 4;
-  const char* nm = getenv("FM_NO_MIDCACHE");  // experiment switch: the midphase list rebuilt at every substep
-  if (nm && nm[0] == '1') M.dbg_flags |= 8;
-  const char* na = getenv("FM_NO_ARROW");  // experiment switch: no block-parallel arrowhead Cholesky
-  if (na && na[0] == '1') M.dbg_flags |= 16;
-  if (na && na[0] == '2') M.dbg_flags |= 32;  // arrowhead factor of the LDS-assembled Hessian
-  const char* ns = getenv("FM_NO_SCATTER");  // experiment switch: per-dof gather of J' f instead of the scatter
-  if (ns && ns[0] == '1') M.dbg_flags |= 64;
-  const char* sf = getenv("FM_SERIAL_FK");  // experiment switch: arm kinematics / RNE on one lane per arm
-  if (sf && sf[0] == '1') M.dbg_flags |= 128;
-  const char* fs = getenv("FM_TWO_PASS_SETUP");  // experiment switch: the warmstart candidates in two row passes
-  if (fs && fs[0] == '1') M.dbg_flags |= 256;
+  M.dbg_flags = h->xflags;
   return M;
+}
+
+// experiment switches of the kernel (A/B probes and the equivalence tests; every default is 0): read from the
+// environment once, at fm_create, and reported on stderr when any is set; "experiment_flags" (fm_set_param) changes
+// them on a live handle for later launches
+static uint32_t read_experiment_flags() {
+  struct Sw {
+    const char* var;
+    char val;
+    uint32_t bit;
+  };
+  static const Sw sw[] = {
+      {"FM_CHOL_LDS", '1', 1},         // sparse LDS Cholesky instead of the register / matrix-core factors
+      {"FM_CHOL_LDS", '2', 2},         // (4,16): the sparse LDS Cholesky instead of the dense matrix-core one
+      {"FM_SERIAL_BOXBOX", '1', 4},    // one lane per box-box pair throughout
+      {"FM_NO_MIDCACHE", '1', 8},      // the midphase list rebuilt at every substep
+      {"FM_NO_ARROW", '1', 16},        // no block-parallel arrowhead Cholesky
+      {"FM_NO_ARROW", '2', 32},        // arrowhead factor of the LDS-assembled Hessian
+      {"FM_NO_SCATTER", '1', 64},      // per-dof gather of J' f instead of the scatter
+      {"FM_SERIAL_FK", '1', 128},      // arm kinematics / RNE on one lane per arm
+      {"FM_TWO_PASS_SETUP", '1', 256}, // the warmstart candidates in two row passes
+  };
+  uint32_t f = 0;
+  for (const Sw& x : sw) {
+    const char* v = getenv(x.var);
+    if (v && v[0] == x.val) f |= x.bit;
+  }
+  if (f) fprintf(stderr, "factorysim: experiment switches active (flags 0x%x)\n", f);
+  return f;
 }
 
 template <typename T>
@@ -637,6 +655,7 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
   h->cfg = *cfg;
   h->device = device;
   h->fp64 = cfg->precision == FM_FP64;
+  h->xflags = read_experiment_flags();
   if (cfg->env_class < FM_ENV_FACTORY || cfg->env_class > FM_ENV_BACKUP_IK_TOGGLE) {
     delete h;
     return set_err(FM_EINVAL, "unknown env_class");
@@ -763,6 +782,11 @@ static double* param_slot(fm_handle* h, const char* name, double* scale) {
 
 int fm_set_param(fm_handle* h, const char* name, double value) {
   if (!h) return set_err(FM_EINVAL, "null handle");
+  if (name && std::string(name) == "experiment_flags") {
+    if (!(value >= 0 && value < 65536 && value == (double)(uint32_t)value)) return set_err(FM_EINVAL, "bad flags");
+    h->xflags = (uint32_t)value;
+    return FM_OK;
+  }
   double scale;
   double* p = param_slot(h, name, &scale);
   if (!p) return set_err(FM_EINVAL, std::string("not a runtime-mutable parameter: ") + (name ? name : "(null)"));
@@ -773,6 +797,10 @@ int fm_set_param(fm_handle* h, const char* name, double value) {
 
 int fm_get_param(const fm_handle* h, const char* name, double* value) {
   if (!h || !value) return set_err(FM_EINVAL, "null argument");
+  if (name && std::string(name) == "experiment_flags") {
+    *value = (double)h->xflags;
+    return FM_OK;
+  }
   double scale;
   double* p = param_slot(const_cast<fm_handle*>(h), name, &scale);
   if (!p) return set_err(FM_EINVAL, std::string("not a runtime-mutable parameter: ") + (name ? name : "(null)"));

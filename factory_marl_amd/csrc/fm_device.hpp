@@ -600,7 +600,7 @@ __device__ __forceinline__ void kb_params(T dt, const T* solref, const T* solimp
 // contact order equals the oracle's pair order whatever order the lanes emitted in.
 template <typename T>
 struct Emit {
-  T* st;         // staging [cap][8]: dist pos(3) n(3)
+  T* st;         // staging [cap][8]: dist pos(3) n(3); pos relative to the pair's anchor (contact_anchor)
   int* keys;     // [cap]
   uint32_t* pw;  // [cap] type-ordered pair word (c1 | c2 << 12 | param << 24)
   int* cnt;
@@ -608,6 +608,7 @@ struct Emit {
   int key;
   uint32_t pair;
   int sub;
+  double o[3];   // the anchor in the kernel frame
   template <typename X>
   __device__ void operator()(X dist, X p0, X p1, X p2, X n0, X n1, X n2) {
     if (sub >= MAXPC) return;
@@ -615,9 +616,9 @@ struct Emit {
     if (s < cap) {
       T* r = st + 8 * s;
       r[0] = (T)dist;
-      r[1] = (T)p0;
-      r[2] = (T)p1;
-      r[3] = (T)p2;
+      r[1] = (T)((double)p0 - o[0]);
+      r[2] = (T)((double)p1 - o[1]);
+      r[3] = (T)((double)p2 - o[2]);
       r[4] = (T)n0;
       r[5] = (T)n1;
       r[6] = (T)n2;
@@ -1092,6 +1093,32 @@ __device__ __forceinline__ void geom_pose_f64(const Model<T>& M, const Ws<T, DIM
   }
 }
 
+// A contact's position is stored relative to its pair's anchor: the centre of the pair's cube (geom 2's body if it
+// is a cube, else geom 1's), otherwise the kernel-frame origin.  The point and the cube's lever arm p - c then keep
+// float precision wherever the cube sits: at the parking spots x = 4..5 m (task_utils.py:31-36, 115-129) float
+// coordinates are 4.8e-7 m apart against 2.3e-6 m resting depths, which turned into spin noise of parked cubes
+template <typename DD>
+__device__ __forceinline__ int anchor_cube(const DD& dm, int kb1, int kb2) {
+  if (kb2 >= 2 && kb2 < 2 + dm.K) return kb2 - 2;
+  if (kb1 >= 2 && kb1 < 2 + dm.K) return kb1 - 2;
+  return -1;
+}
+template <typename T, typename DIM>
+__device__ __forceinline__ void contact_anchor(const Ws<T, DIM>& w, int ak, double* o) {
+  if (ak < 0) {
+    o[0] = o[1] = o[2] = 0.0;
+    return;
+  }
+  const double* c = w.qd() + 1 + 7 * ak;
+  o[0] = c[0];
+  o[1] = c[1];
+  o[2] = c[2] - zshift<T>();
+}
+template <typename T, typename DIM, typename E>
+__device__ __forceinline__ void set_anchor(const Ws<T, DIM>& w, const DIM& dm, int kb1, int kb2, E& emit) {
+  contact_anchor(w, anchor_cube(dm, kb1, kb2), emit.o);
+}
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>& w, const uint32_t* list, int n) {
   const DIM dm(M.dm);
@@ -1104,6 +1131,7 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
     const int kb1 = (gi1 >> 8) & 255, kb2 = (gi2 >> 8) & 255;
     const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
     Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
+    set_anchor(w, dm, kb1, kb2, emit);
     double p1[3], R1[9], h1[3], p2[3], R2[9], h2[3];
     geom_pose_f64(M, w, c2, kb2, p2, R2, h2);
     if (t1 == GC_PLANE) {
@@ -1133,6 +1161,7 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
   const T* x2 = w.gx() + 4 * c2;
   int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
   Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
+  set_anchor(w, dm, kb1, kb2, emit);
   T p1[3] = {x1[0], x1[1], x1[2]}, p2[3] = {x2[0], x2[1], x2[2]};
   if (t1 == GC_PLANE) {
     if (t2 == GC_SPHERE) {
@@ -1234,7 +1263,8 @@ __device__ __forceinline__ void narrow_bb_parallel(const Model<T>& M, const Ws<T
     sat.best_edge = eo;
     const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
     Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
-    const bool edge = sat.edge_id >= 0 && sat.best_edge < NP(0.95) * sat.best_face;
+    set_anchor(w, dm, kb1, kb2, emit);
+    const bool edge =sat.edge_id >= 0 && sat.best_edge < NP(0.95) * sat.best_face;
     if (live && !sep && edge && ax == 0) np_box_box_finish(p1, R1, h1, p2, R2, h2, sat, emit);  // one point
     // face contact: candidates c = ax and 16 + ax (ax < 8) of the serial order on the pair's 16 lanes; the k-th
     // contact in that order (rank by ballot prefix) takes index k within the pair, as the serial loop numbers them
@@ -2151,9 +2181,29 @@ __device__ __forceinline__ void arm_jac_col(const Ws<T, DIM>& w, int arm, int b,
   }
 }
 
-// translational Jacobian column j (tree-local) of point p on kernel body kb in its tree
+// the point a contact's Jacobian columns on kernel body kb need (p = the contact point relative to its anchor o,
+// contact_anchor): a cube's lever arm p - c formed as p + (o - c) with o - c in float64 (exactly 0 for the anchor
+// cube itself); an arm body's point in the kernel frame
 template <typename T, typename DIM>
-__device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T, DIM>& w, int kb, int j, const T* p, T* col) {
+__device__ __forceinline__ void body_jac_point(const Model<T>& M, const Ws<T, DIM>& w, int kb, const T* p,
+                                               const double* o, T* pt) {
+  const DIM dm(M.dm);
+  if (kb >= 2 && kb < 2 + dm.K) {
+    const double* c = w.qd() + 1 + 7 * (kb - 2);
+    pt[0] = p[0] + (T)(o[0] - c[0]);
+    pt[1] = p[1] + (T)(o[1] - c[1]);
+    pt[2] = p[2] + (T)(o[2] - (c[2] - zshift<T>()));
+  } else {
+    pt[0] = (T)(o[0] + (double)p[0]);
+    pt[1] = (T)(o[1] + (double)p[1]);
+    pt[2] = (T)(o[2] + (double)p[2]);
+  }
+}
+
+// translational Jacobian column j (tree-local) on kernel body kb in its tree; pt from body_jac_point (a cube's lever
+// arm, an arm body's point)
+template <typename T, typename DIM>
+__device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T, DIM>& w, int kb, int j, const T* pt, T* col) {
   const DIM dm(M.dm);
   if (kb == 1) {
     col[0] = 0;
@@ -2166,12 +2216,11 @@ __device__ __forceinline__ void body_jac_col(const Model<T>& M, const Ws<T, DIM>
       col[j] = 1;
     } else {
       const T* R = w.cR() + 9 * k;
-      const T* c = w.q() + 1 + 7 * k;
       T ax[3] = {R[j - 3], R[3 + j - 3], R[6 + j - 3]};
-      T rel[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
-      cross3(ax, rel, col);
+      cross3(ax, pt, col);
     }
   } else {
+    const T* p = pt;
     int arm = (kb - 2 - dm.K) / 10, b = (kb - 2 - dm.K) % 10;
     arm_jac_col(w, arm, b, j, p, col);
   }
@@ -2382,6 +2431,11 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     int nda = ta >= 0 ? tree_nd(dm, ta) : 0;
     int ndb = tb >= 0 ? tree_nd(dm, tb) : 0;
     const T p[3] = {cr[CR_POS], cr[CR_POS + 1], cr[CR_POS + 2]};
+    double o[3];
+    contact_anchor(w, anchor_cube(dm, kb1, kb2), o);
+    T pt1[3], pt2[3];
+    body_jac_point(M, w, kb1, p, o, pt1);
+    body_jac_point(M, w, kb2, p, o, pt2);
     T* J = cr + CR_J;
     for (int blk = 0; blk < 2; blk++) {
       int t = blk == 0 ? ta : tb;
@@ -2392,12 +2446,12 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
         T col[3] = {0, 0, 0};
         if (tr2 == t) {
           T c2v[3];
-          body_jac_col(M, w, kb2, j, p, c2v);
+          body_jac_col(M, w, kb2, j, pt2, c2v);
           for (int k = 0; k < 3; k++) col[k] += c2v[k];
         }
         if (tr1 == t) {
           T c1v[3];
-          body_jac_col(M, w, kb1, j, p, c1v);
+          body_jac_col(M, w, kb1, j, pt1, c1v);
           for (int k = 0; k < 3; k++) col[k] -= c1v[k];
         }
         for (int r = 0; r < 3; r++) J[r * CJ + col0 + j] = dot3(f + 3 * r, col);
@@ -2503,7 +2557,10 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     const int nh = DIM::MAXC == WAVE ? 1 : (dm.maxcon + WAVE - 1) / WAVE;
 #pragma unroll
     for (int h = 0; h < DIM::MAXC / WAVE; h++) {
-      if (h >= nh) break;
+      if (h >= nh) {  // words past the scene's contact capacity hold no contact (readers scan all MAXC / 64)
+        for (int t = LANE; t < dm.ntree; t += WAVE) w.tmask()[h * dm.ntree + t] = 0ull;
+        continue;
+      }
       int ta = -2, tb = -2;
       if (LANE + WAVE * h < ncon) {
         ta = w.ci()[4 * (LANE + WAVE * h) + 1];
@@ -5240,7 +5297,10 @@ __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L
         r[0] = M.geom_i[4 * (ci[0] & 4095)];
         r[1] = M.geom_i[4 * ((ci[0] >> 12) & 4095)];
         r[2] = cr[CR_DIST];
-        for (int k = 0; k < 3; k++) r[3 + k] = (double)cr[CR_POS + k] + (k == 2 ? zs : 0.0);
+        double o[3];
+        contact_anchor(w, anchor_cube(dm, (w.ginfo()[ci[0] & 4095] >> 8) & 255, (w.ginfo()[(ci[0] >> 12) & 4095] >> 8) & 255),
+                       o);
+        for (int k = 0; k < 3; k++) r[3 + k] = o[k] + (double)cr[CR_POS + k] + (k == 2 ? zs : 0.0);
         for (int k = 0; k < 9; k++) r[6 + k] = cr[CR_FR + k];
         r[15] = cr[CR_MU];
         r[16] = cr[CR_D];

@@ -74,6 +74,18 @@ class RankContext:
     def sum_over_ranks(self, x):
         return reduce_over_ranks(x, "sum", self.device if self.backend == "nccl" else None)
 
+    def gather_rank_times(self, wall, kernel_ms):
+        """every rank's own timed-region wall time and average kernel time, gathered to every rank (per-rank
+        imbalance in an N-GPU line); a one-element list at N=1"""
+        mine = {"rank": self.rank, "wall_s": round(float(wall), 4), "kernel_ms": round(float(kernel_ms), 4)}
+        if not self.distributed:
+            return [mine]
+        import torch.distributed as dist
+
+        out = [None] * self.world
+        dist.all_gather_object(out, mine)
+        return out
+
     def close(self):
         if self.distributed:
             import torch.distributed as dist

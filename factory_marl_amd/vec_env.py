@@ -17,6 +17,7 @@ constructors resolve them (``environments.resolve_kwargs``: required ProgressRew
 TypeError on unknown keywords).
 """
 import ctypes as C
+import math
 import time
 
 import numpy as np
@@ -37,6 +38,11 @@ ENV_CLASSES = {
 TOGGLE_CLASSES = envs.TOGGLE_CLASSES
 
 # env attributes with a value on the GPU path (base_env.py:133-147, environments.py:276-282):
+# the kernel's experiment switches (fm_api.hip read_experiment_flags): (environment variable, value) -> flag bit
+EXPERIMENT_FLAGS = {("FM_CHOL_LDS", "1"): 1, ("FM_CHOL_LDS", "2"): 2, ("FM_SERIAL_BOXBOX", "1"): 4,
+                    ("FM_NO_MIDCACHE", "1"): 8, ("FM_NO_ARROW", "1"): 16, ("FM_NO_ARROW", "2"): 32,
+                    ("FM_NO_SCATTER", "1"): 64, ("FM_SERIAL_FK", "1"): 128, ("FM_TWO_PASS_SETUP", "1"): 256}
+
 # global scalars of the handle (fm_set_param), per-arena values of the state record, fixed at creation
 RUNTIME_PARAMS = ("pt_time", "initial_conveyor_speed", "conveyor_acceleration", "force_contact_threshold",
                   "spawn_freq_increase", "init_spawn_freq", "gripper_to_closest_cube_reward_factor",
@@ -268,6 +274,15 @@ class FactoryVecEnv:
             return [indices]
         return [int(i) for i in indices]
 
+    def set_experiment(self, setting=""):
+        """the kernel's experiment switches on this live handle (A/B probes and equivalence tests only):
+        "FM_NO_ARROW=1 FM_NO_SCATTER=1" (EXPERIMENT_FLAGS) for the launches queued after the call; "" clears all"""
+        flags = 0
+        for kv in (setting or "").split():
+            k, v = kv.split("=")
+            flags |= EXPERIMENT_FLAGS[(k, v)]
+        _lib.check(self._L.fm_set_param(self._h, b"experiment_flags", float(flags)))
+
     def get_param(self, name):
         v = C.c_double()
         _lib.check(self._L.fm_get_param(self._h, name.encode(), C.byref(v)))
@@ -320,7 +335,8 @@ class FactoryVecEnv:
         idx = self._indices(indices)
         if name in RUNTIME_PARAMS:
             v = float(np.asarray(value).reshape(-1)[0])
-            if len(set(idx)) != self.num_envs and v != self.get_param(name):
+            # init_spawn_freq is held per arm (v / A) and read back as (v / A) * A: compare to rounding
+            if len(set(idx)) != self.num_envs and not math.isclose(v, self.get_param(name), rel_tol=1e-12, abs_tol=0.0):
                 raise ValueError(f"{name} is one value for all {self.num_envs} arenas of the batch: set it on every env")
             _lib.check(self._L.fm_set_param(self._h, name.encode(), v))
             return

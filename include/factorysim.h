@@ -114,7 +114,9 @@ int fm_sync(fm_handle* h);
  * "gripper_to_closest_cube_reward_factor", "closest_cube_to_bucket_reward_factor",
  * "small_action_norm_reward_factor", "base_reward".  Global to the handle; launches queued after the call use the
  * new value.  control_frequency (frame_skip), num_arms, max_num_objects and seeds are fixed at fm_create.
- * Per-arena dynamic values (play_time, conveyor_speed, spawn_freq) live in the state record (fm_set_state). */
+ * Per-arena dynamic values (play_time, conveyor_speed, spawn_freq) live in the state record (fm_set_state).
+ * "experiment_flags": the kernel's experiment switches (A/B probes and equivalence tests only; 0 in production),
+ * initialised once at fm_create from FM_* environment variables. */
 int fm_set_param(fm_handle* h, const char* name, double value);
 int fm_get_param(const fm_handle* h, const char* name, double* value);
 

@@ -41,13 +41,13 @@ def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights
     return np.stack(recs), np.stack(acts), outs
 
 
-def restep_at_tolerance(oracle, A, K, trajectory, tol):
+def restep_at_tolerance(oracle, A, K, trajectory, tol, env_class="AllFullRLProgressRewardEnv"):
     """the same states and actions, stepped by an oracle whose Newton stops at `tol` (MuJoCo's default opt.tolerance
     is 1e-8; the oracle's own is 1e-12): the expected outputs of a MuJoCo-tolerance solve"""
     from factory_marl_amd import state as st
 
     recs, acts, _ = trajectory
-    p = oracle.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4))
+    p = oracle.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4), env_class=env_class)
     p.reset()
     L = oracle.lib()
     outs = []
@@ -85,6 +85,24 @@ def state_err(A, K, got_dbl, ref_dbl):
     qd = np.abs(got_dbl[:nq] - ref_dbl[:nq]) / np.maximum(np.abs(ref_dbl[:nq]), 1.0)
     vd = np.abs(got_dbl[nq:nq + nv] - ref_dbl[nq:nq + nv]) / np.maximum(np.abs(ref_dbl[nq:nq + nv]), 0.1)
     return qd, vd
+
+
+def entry_name(A, K, j, dbl):
+    """a state entry's name: qpos / qvel index, its body (belt, cube k with its position, arm a joint d)"""
+    nq = 1 + 7 * K + 9 * A
+    isq = j < nq
+    i = j if isq else j - nq
+    per = 7 if isq else 6
+    if i == 0:
+        body = "belt"
+    elif i < 1 + per * K:
+        k = (i - 1) // per
+        x, y, z = dbl[1 + 7 * k:4 + 7 * k]
+        body = f"cube {k} comp {(i - 1) % per} at ({x:.2f},{y:.2f},{z:.3f})"
+    else:
+        a, d = divmod(i - 1 - per * K, 9)
+        body = f"arm {a} dof {d}"
+    return f"{'qpos' if isq else 'qvel'}[{i}] ({body})"
 
 
 def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv", verbose_tol=None, **kw):
@@ -125,7 +143,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
         err_steps.append(s)
         if verbose_tol is not None and errs[-1] > verbose_tol:
             j = int(np.argmax(np.concatenate([qd, vd])))
-            print(f"  step {s}: worst {'qpos' if j < nq else 'qvel'}[{j if j < nq else j - nq}] "
+            print(f"  step {s}: worst {entry_name(A, K, j, o['dbl'])} "
                   f"rel {errs[-1]:.2e} ref {o['dbl'][j]:.6g} got {gd[j]:.6g}; cubes {o['info']['num_obj']}")
         rew_err.append(abs(rew[s] - o["reward"]))
         obs_err.append(np.abs(obs[s] - o["obs"]).max())

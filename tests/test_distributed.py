@@ -124,3 +124,32 @@ def test_bench_single_rank_and_config4_split():
     assert d["n_gpus"] == 1 and d["rank_arenas"] == [[0, 4096]]
     d4 = _run_bench("--gpus", "2", "--workload", "config4")
     assert d4["scaling"] == "strong" and d4["rank_arenas"] == [[0, 65536], [65536, 131072]]
+
+
+def test_bench_watchdog_stops_a_stalled_job():
+    """`bench.py --gpus 2` with a rank that never reaches the collectives (it sleeps past the deadline): the parent
+    stops every rank at the deadline, names the unfinished ranks on stderr and exits non-zero"""
+    import json
+    import subprocess
+    import sys
+    import time
+
+    import bench
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run", "--gpus", "2", "--deadline", "20",
+                          "--stall-rank", "1", "--stall-seconds", "600"], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == bench.WATCHDOG_RC, (out.returncode, out.stderr[-2000:])
+    assert time.monotonic() - t0 < 120
+    rec = [json.loads(ln) for ln in out.stderr.splitlines() if ln.startswith('{"error"')]
+    assert rec and rec[0]["error"] == "watchdog" and 1 in rec[0]["ranks_unfinished"], out.stderr[-2000:]
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]  # no result line from a stopped job
+
+
+def test_bench_line_carries_per_rank_times():
+    d = _run_bench("--gpus", "2", "--steps", "10")
+    assert [r["rank"] for r in d["per_rank"]] == [0, 1]
+    assert [r["wall_s"] for r in d["per_rank"]] == [1.0, 1.5]

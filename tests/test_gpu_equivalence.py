@@ -1,4 +1,5 @@
-"""The kernel's exact reformulations against their straightforward forms, on the GPU (switches read at each launch):
+"""The kernel's exact reformulations against their straightforward forms, on the GPU (experiment switches set on the
+live handle, FactoryVecEnv.set_experiment):
 
 * the cached midphase (a body-pair list of an inflated test reused across substeps) against a rebuild at every
   substep (FM_NO_MIDCACHE=1): the contact set is the same by construction, so the trajectories are bit-identical;
@@ -22,35 +23,28 @@ def _have_gpu():
     return torch.cuda.is_available()
 
 
-def _run(A, K, n, steps, switch, precision="fp32", env_class="AllFullRLProgressRewardEnv"):
+def _run(A, K, n, steps, switch, precision="fp32", env_class="AllFullRLProgressRewardEnv", value="1"):
     from factory_marl_amd import FactoryVecEnv
     from factory_marl_amd.environments import run_kwargs
 
-    old = os.environ.pop(switch, None)
-    try:
-        env = FactoryVecEnv(n, env_class=env_class, env_kwargs=run_kwargs(env_class, num_arms=A, max_num_objects=K,
-                                                                          seed=42),
-                            precision=precision, seeds=42 + np.arange(n), return_numpy=False)
-        env.reset()
-        s0 = env.get_state()  # both runs start from this record (reset() continues the TaskManager RNG)
-        g = torch.Generator(device=env.device)
-        g.manual_seed(5)
-        acts = [torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1 for _ in range(steps)]
-        out = []
-        for on in (False, True):
-            env.set_state(s0)
-            if on:
-                os.environ[switch] = "1" if switch != "FM_CHOL_LDS" else "2"
-            for a in acts:
-                env.step_tensors(a)
-            env.sync()
-            os.environ.pop(switch, None)
-            out.append(env.get_state())
-        env.close()
-        return out
-    finally:
-        if old is not None:
-            os.environ[switch] = old
+    env = FactoryVecEnv(n, env_class=env_class, env_kwargs=run_kwargs(env_class, num_arms=A, max_num_objects=K,
+                                                                      seed=42),
+                        precision=precision, seeds=42 + np.arange(n), return_numpy=False)
+    env.reset()
+    s0 = env.get_state()  # both runs start from this record (reset() continues the TaskManager RNG)
+    g = torch.Generator(device=env.device)
+    g.manual_seed(5)
+    acts = [torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1 for _ in range(steps)]
+    out = []
+    for on in (False, True):
+        env.set_state(s0)
+        env.set_experiment(f"{switch}={value}" if on else "")
+        for a in acts:
+            env.step_tensors(a)
+        env.sync()
+        out.append(env.get_state())
+    env.close()
+    return out
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
@@ -102,13 +96,12 @@ def test_dense_cholesky_agrees_with_sparse_4x16():
     s0 = env.get_state()
     a = (torch.rand(n, A, device=env.device, generator=g) < 0.5).float()
     res = []
-    for mode in ("0", "2"):
-        os.environ["FM_CHOL_LDS"] = mode
+    for mode in (None, "2"):
+        env.set_experiment(f"FM_CHOL_LDS={mode}" if mode else "")
         env.set_state(s0)
         env.step_tensors(a)
         env.sync()
         res.append(env.get_state())
-    os.environ.pop("FM_CHOL_LDS", None)
     env.close()
     errs = []
     for i in range(n):
@@ -120,3 +113,55 @@ def test_dense_cholesky_agrees_with_sparse_4x16():
     print(f"dense vs sparse Cholesky, one env-step from 128 states: median {np.median(errs):.2e}, "
           f"within 1e-4 {np.mean(errs <= 1e-4):.1%}, worst {errs.max():.2e}")
     assert np.mean(errs <= 1e-4) >= 0.9 and np.median(errs) <= 1e-5
+
+
+def _one_step(A, K, n, pre, switch, value="1", precision="fp32"):
+    """`pre` random-action env-steps from reset (n arenas of their own seeds: diverse states), then one env-step from
+    that record with the switch off and on; returns the per-arena worst relative state difference (SURVEY metric)"""
+    import parity_util as pu
+    from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd import state as st
+    from factory_marl_amd.environments import run_kwargs
+
+    env = FactoryVecEnv(n, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=A, max_num_objects=K, seed=42),
+                        precision=precision, seeds=42 + np.arange(n), return_numpy=False)
+    env.reset()
+    g = torch.Generator(device=env.device)
+    g.manual_seed(11)
+    for _ in range(pre):
+        env.step_tensors(torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1)
+    env.sync()
+    s0 = env.get_state()
+    a = torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1
+    res = []
+    for on in (False, True):
+        env.set_experiment(f"{switch}={value}" if on else "")
+        env.set_state(s0)
+        env.step_tensors(a)
+        env.sync()
+        res.append(env.get_state())
+    env.close()
+    errs = np.array([max(m.max() for m in pu.state_err(A, K, st.unpack(A, K, res[0][i])[0],
+                                                       st.unpack(A, K, res[1][i])[0])) for i in range(n)])
+    return errs
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("A,K", [(2, 8), (2, 10)])
+def test_two_pass_arrowhead_agrees_with_bordered_factor(A, K):
+    """fp32 (2,8) / (2,10): the two-pass arrowhead block factor (chol_arrow2_rl, the default on arrowhead substeps)
+    against the bordered register + matrix-core Schur factor (FM_NO_ARROW=1) -- the same Cholesky of the same
+    Hessian in another summation order: one env-step from 256 diverse states agrees to float32 rounding"""
+    errs = _one_step(A, K, 256, 60, "FM_NO_ARROW")
+    print(f"({A},{K}) two-pass arrowhead vs bordered factor, one env-step from 256 states: median {np.median(errs):.2e}, "
+          f"99th pct {np.quantile(errs, 0.99):.2e}, worst {errs.max():.2e}")
+    assert np.median(errs) <= 1e-6 and np.mean(errs <= 1e-5) >= 0.99 and errs.max() <= 1e-4
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_one_pass_warmstart_products_are_exact(precision):
+    """(2,4): both warmstart candidates' row products in one pass (rows_eval2) against two separate passes
+    (FM_TWO_PASS_SETUP=1): the same products per row, so 40 env-steps of 256 arenas are bit-identical"""
+    a, b = _run(2, 4, 256, 40, "FM_TWO_PASS_SETUP", precision=precision)
+    assert np.array_equal(a, b)

@@ -19,10 +19,7 @@ from factory_marl_amd.environments import run_kwargs  # noqa: E402
 def run(env, s0, acts, mode):
     """mode "" = default (Hessian assembled in the arrowhead factor's registers), "1" = general register Cholesky,
     "2" = arrowhead factor of the LDS-assembled Hessian"""
-    if mode:
-        os.environ["FM_NO_ARROW"] = mode
-    else:
-        os.environ.pop("FM_NO_ARROW", None)
+    env.set_experiment(f"FM_NO_ARROW={mode}" if mode else "")
     env.set_state(s0)
     env.sync()
     t0 = time.perf_counter()
@@ -65,7 +62,6 @@ def main():
                          ms_per_step_general=1e3 * tg / args.steps)
         print(prec, out[prec], flush=True)
         env.close()
-    os.environ.pop("FM_NO_ARROW", None)
     print(json.dumps(out))
 
 

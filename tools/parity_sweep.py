@@ -4,6 +4,7 @@ solver setting, one JSON line per trajectory (tests/parity_util.summary + the se
 
 usage: FACTORYSIM_LIB=path python tools/parity_sweep.py --prec fp32 [--tol 1e-9] [--tag name]
            [--traj A,K,T,seed[,EnvClass[,oracle_tol]] ...]   (default: 2,4,96,7  2,4,300,21  2,8,300,5  2,10,250,9)
+       python tools/parity_sweep.py --make-only --workers 8 --traj ...   (oracle rollouts into the cache, no GPU)
 Trajectories are cached as .npz under gpurun_out/traj/ (or $FM_TRAJ_CACHE: a cache made in the container travels
 with the tree) so several processes share one oracle rollout.
 """
@@ -33,7 +34,9 @@ def load_traj(A, K, T, seed, env_class="AllFullRLProgressRewardEnv",
         tag += f"_tol{oracle_tol:g}"
     f = os.path.join(cache, f"traj_{A}_{K}_{T}_{seed}{tag}.npz")
     if oracle_tol > 0 and not os.path.exists(f):
-        raise FileNotFoundError(f + " (make it with tools/tolerance_floor.py --make-traj)")
+        # the tight oracle's states and actions, restepped at the given Newton tolerance
+        trj = pu.restep_at_tolerance(po, A, K, load_traj(A, K, T, seed, env_class, cache), oracle_tol, env_class)
+        _save(f, *trj)
     if os.path.exists(f):
         z = np.load(f)
         meta = json.load(open(f[:-4] + ".json"))
@@ -43,12 +46,31 @@ def load_traj(A, K, T, seed, env_class="AllFullRLProgressRewardEnv",
                              info=meta["info"][s], dbl=z["dbl"][s], ints=z["ints"][s], rng=z["rng"][s]))
         return z["recs"], z["acts"], outs
     recs, acts, outs = pu.rollout(po, A, K, T, seed_actions=seed, env_class=env_class)
+    _save(f, recs, acts, outs)
+    return recs, acts, outs
+
+
+def _save(f, recs, acts, outs):
     np.savez(f, recs=recs, acts=acts, obs=np.stack([o["obs"] for o in outs]),
              reward=np.array([o["reward"] for o in outs]), term=np.array([o["term"] for o in outs]),
              dbl=np.stack([o["dbl"] for o in outs]), ints=np.stack([o["ints"] for o in outs]),
              rng=np.stack([o["rng"] for o in outs]))
     json.dump(dict(info=[o["info"] for o in outs]), open(f[:-4] + ".json", "w"))
-    return recs, acts, outs
+
+
+def _parse(spec):
+    f = spec.split(",")
+    A, K, T, seed = (int(x) for x in f[:4])
+    env_class = f[4] if len(f) > 4 and f[4] else "AllFullRLProgressRewardEnv"
+    otol = float(f[5]) if len(f) > 5 and f[5] else 0.0
+    return A, K, T, seed, env_class, otol
+
+
+def _make(spec):
+    A, K, T, seed, env_class, otol = _parse(spec)
+    t0 = time.time()
+    load_traj(A, K, T, seed, env_class, oracle_tol=otol)
+    return f"{spec}: {time.time() - t0:.1f} s"
 
 
 def main():
@@ -58,17 +80,30 @@ def main():
     ap.add_argument("--iters", type=int, default=0)
     ap.add_argument("--tag", default="")
     ap.add_argument("--traj", nargs="*", default=["2,4,96,7", "2,4,300,21", "2,8,300,5", "2,10,250,9"])
+    ap.add_argument("--make-only", action="store_true", help="oracle rollouts into the cache only (no GPU)")
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--verbose-tol", type=float, default=None, help="print the worst entry of steps above this")
     args = ap.parse_args()
     po.build()
+    if args.make_only:
+        # tight trajectories first (the tolerance variants restep their states)
+        specs = sorted(set(args.traj), key=lambda s: len(s.split(",")))
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(max(1, args.workers)) as pool:
+            tight = sorted({",".join(s.split(",")[:4] + [s.split(",")[4]] if len(s.split(",")) > 4 and s.split(",")[4]
+                                     else s.split(",")[:4]) for s in specs})
+            for out in pool.imap_unordered(_make, tight):
+                print(out, flush=True)
+            for out in pool.imap_unordered(_make, [s for s in specs if len(s.split(",")) > 5]):
+                print(out, flush=True)
+        return
     for spec in args.traj:
-        f = spec.split(",")
-        A, K, T, seed = (int(x) for x in f[:4])
-        env_class = f[4] if len(f) > 4 and f[4] else "AllFullRLProgressRewardEnv"
-        otol = float(f[5]) if len(f) > 5 else 0.0
+        A, K, T, seed, env_class, otol = _parse(spec)
         t0 = time.time()
         traj = load_traj(A, K, T, seed, env_class, oracle_tol=otol)
         t1 = time.time()
-        r = pu.compare(traj, args.prec, A, K, env_class, solver_tolerance=args.tol, solver_iterations=args.iters)
+        r = pu.compare(traj, args.prec, A, K, env_class, verbose_tol=args.verbose_tol, solver_tolerance=args.tol,
+                       solver_iterations=args.iters)
         s = pu.summary(r)
         s.update(tag=args.tag, lib=os.path.basename(os.environ.get("FACTORYSIM_LIB", "libfactorysim.so")),
                  prec=args.prec, tol=args.tol,

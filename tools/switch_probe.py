@@ -1,4 +1,4 @@
-"""A/B of the kernel's experiment switches (environment variables read at each launch, fm_api.hip make_model) on the
+"""A/B of the kernel's experiment switches (FactoryVecEnv.set_experiment on the live handle) on the
 (2,4) scene: the same states stepped with the same actions under each switch setting; reports per setting the
 arenas whose full state record differs bitwise from the first setting's, and the time per env-step.
 usage: python tools/switch_probe.py [--arenas N] [--steps K] -- "" FM_NO_SCATTER=1 "FM_NO_ARROW=1 FM_NO_SCATTER=1"
@@ -16,19 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from factory_marl_amd import FactoryVecEnv  # noqa: E402
 from factory_marl_amd.environments import run_kwargs  # noqa: E402
 
-SWITCHES = ("FM_NO_ARROW", "FM_NO_SCATTER", "FM_SERIAL_FK", "FM_TWO_PASS_SETUP", "FM_NO_MIDCACHE", "FM_SERIAL_BOXBOX", "FM_CHOL_LDS")
-
-
-def apply(setting):
-    for k in SWITCHES:
-        os.environ.pop(k, None)
-    for kv in setting.split():
-        k, v = kv.split("=")
-        os.environ[k] = v
-
-
 def run(env, s0, acts, setting):
-    apply(setting)
+    env.set_experiment(setting)
     env.set_state(s0)
     env.sync()
     t0 = time.perf_counter()
