@@ -64,7 +64,7 @@ EXPORTED = [
     "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
     "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile", "fm_scene_mjcf",
-    "fm_render", "fm_render_ngeom", "fm_set_param", "fm_get_param",
+    "fm_render", "fm_render_ngeom", "fm_set_param", "fm_get_param", "fm_num_counters",
 ]
 
 _LIB = None
@@ -122,8 +122,16 @@ def load():
     L.fm_set_param.restype = I
     L.fm_get_param.argtypes = [P, C.c_char_p, C.POINTER(C.c_double)]
     L.fm_get_param.restype = I
+    if hasattr(L, "fm_num_counters"):
+        L.fm_num_counters.argtypes = []
+        L.fm_num_counters.restype = I
     _LIB = L
     return L
+
+
+def num_counters(L):
+    """per-arena diagnostic counters of the library (fm_num_counters; libraries before it exported 8)"""
+    return L.fm_num_counters() if hasattr(L, "fm_num_counters") else 8
 
 
 def check(rc):

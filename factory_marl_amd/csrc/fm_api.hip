@@ -18,6 +18,12 @@
 
 namespace fm {
 template <typename T, int A, int K>
+hipError_t rerun_set_attr();
+template <typename T, int A, int K>
+Lay rerun_layout();
+template <typename T, int A, int K>
+void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik);
+template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes);
 template <typename T, int A, int K>
 void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStream_t stream, bool ik);
@@ -95,7 +101,13 @@ struct fm_handle {
   Lay lay_step{};  // workspace layout of the env-step kernel in use
   bool spill = false;          // DimsSpill: Hessian + contact records in per-arena global scratch (fp64, > 160 KiB)
   uint32_t xflags = 0;         // experiment switches (Model::dbg_flags): read once at fm_create, fm_set_param
-  char* spill_buf = nullptr;   // [N][lay.gtotal]
+  // the benchmark scene's lossless contacts: [1 + N] rerun list of the 64-contact launch (fm_dev.hpp State::rerun),
+  // the IK classes' record backup, the wide kernel's layout
+  int32_t* rerun = nullptr;
+  char* bak = nullptr;
+  Lay lay_rerun{};
+  char* spill_buf = nullptr;   // [N][spill_stride]
+  long long spill_stride = 0;  // Lay::gtotal of the spill layout in use (runtime fp64 (4,16); FM_SPILL24 builds)
 };
 
 template <typename T>
@@ -182,6 +194,7 @@ static Model<T> make_model(const fm_handle* h) {
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
   M.dbg_flags = h->xflags;
+  M.ovf_abort = 0;
   return M;
 }
 
@@ -204,6 +217,8 @@ static uint32_t read_experiment_flags() {
       {"FM_NO_SCATTER", '1', 64},      // per-dof gather of J' f instead of the scatter
       {"FM_SERIAL_FK", '1', 128},      // arm kinematics / RNE on one lane per arm
       {"FM_TWO_PASS_SETUP", '1', 256}, // the warmstart candidates in two row passes
+      {"FM_FORCE_RERUN", '1', 512},    // (2,4): every env-step abandoned at its first stage and run by the wide kernel
+      {"FM_NO_RERUN", '1', 1024},      // (2,4): contacts above 64 cut (counted), no wide rerun
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {
@@ -225,7 +240,7 @@ static State<T> make_state(const fm_handle* h) {
   S.cost = h->cost;
   S.order = h->order;
   S.spill = h->spill_buf;
-  S.spill_stride = h->spill ? h->lay.gtotal : 0;
+  S.spill_stride = h->spill_stride;
   return S;
 }
 
@@ -386,6 +401,7 @@ static int create_typed(fm_handle* h) {
       h->lay = lds_layout(d, sizeof(T), true);
       if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
       h->spill = true;
+      h->spill_stride = h->lay.gtotal;
       HIPCHK(hipMalloc((void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay.gtotal));
       h->allocs.push_back(h->spill_buf);
       HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, DimsSpill>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -427,6 +443,23 @@ static int create_typed(fm_handle* h) {
 #undef X
   }
   (void)idx;
+  if (h->fixed >= 0 && h->lay_step.spill) {  // FM_SPILL24 experiment builds: the fixed scene's global scratch
+    h->spill_stride = h->lay_step.gtotal;
+    HIPCHK(hipMalloc((void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay_step.gtotal));
+    h->allocs.push_back(h->spill_buf);
+  }
+  // the benchmark scene at its 64-contact capacity: an env-step with a stage above it is rerun by the wide kernel
+  if (h->fixed >= 0 && FixedDims<2, 4>::matches(d) && d.maxcon == MAXCON) {
+    HIPCHK((rerun_set_attr<T, 2, 4>()));
+    h->lay_rerun = rerun_layout<T, 2, 4>();
+    HIPCHK(hipMalloc((void**)&h->rerun, (N + 1) * sizeof(int32_t)));
+    h->allocs.push_back(h->rerun);
+    HIPCHK(hipMemset(h->rerun, 0, (N + 1) * sizeof(int32_t)));
+    if (h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS) {
+      HIPCHK(hipMalloc((void**)&h->bak, N * (8 * (size_t)d.dbl_stride + 4 * (size_t)d.int_stride)));
+      h->allocs.push_back(h->bak);
+    }
+  }
   if (h->fixed < 0) {
     h->lay_step = h->lay;
     HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -530,9 +563,23 @@ __global__ void __launch_bounds__(1024) lpt_order_kernel(const uint32_t* __restr
   for (int i = t; i < n; i += (int)blockDim.x) order[atomicAdd(&hist[bucket(i)], 1u)] = i;
 }
 
+// the wide-capacity rerun of the arenas the 64-contact launch abandoned (one workgroup per arena of the handle;
+// the ones past the list's count exit at once)
+template <typename T>
+static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik) {
+  StepParams<T> pr = pd;
+  pr.L = h->lay_rerun;
+  pr.S.order = nullptr;
+  pr.S.rerun = h->rerun;
+  pr.S.bak = h->bak;
+  rerun_launch<T, 2, 4>(pr, h->dm.N, h->stream, ik);
+}
+
 template <typename T>
 static void launch_step(fm_handle* h, const StepIO& io) {
   if (h->order) hipLaunchKernelGGL(lpt_order_kernel, dim3(1), dim3(1024), 0, h->stream, h->cost, h->order, h->dm.N);
+  const bool rerun = h->rerun && !(h->xflags & 1024);
+  if (rerun) (void)hipMemsetAsync(h->rerun, 0, sizeof(int32_t), h->stream);
   const StepParams<T> pd{make_model<T>(h), make_state<T>(h), h->lay, io};
   dim3 grid(h->dm.N), block(WAVE);
   const bool ik = h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS;
@@ -541,7 +588,13 @@ static void launch_step(fm_handle* h, const StepIO& io) {
   if (h->fixed == idx) {                                                                               \
     StepParams<T> pf = pd;                                                                             \
     pf.L = h->lay_step;                                                                                \
+    if (rerun) {                                                                                       \
+      pf.M.ovf_abort = 1;                                                                              \
+      pf.S.rerun = h->rerun;                                                                           \
+      pf.S.bak = h->bak;                                                                               \
+    }                                                                                                  \
     fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream, ik);                              \
+    if (rerun) launch_rerun<T>(h, pd, ik);                                                             \
     return;                                                                                            \
   }                                                                                                    \
   idx++;
@@ -807,6 +860,8 @@ int fm_get_param(const fm_handle* h, const char* name, double* value) {
   *value = *p * scale;
   return FM_OK;
 }
+
+int fm_num_counters(void) { return FM_NCTR; }
 
 int fm_sync(fm_handle* h) {
   if (!h) return set_err(FM_EINVAL, "null handle");

@@ -62,6 +62,7 @@ struct Dims {
   static constexpr bool spill = false;  // Hessian + contact records in LDS (see DimsSpill)
   static constexpr bool midcache = false;  // cached midphase (FixedDims of the large scenes)
   static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
+  static constexpr bool rerun = false;      // see FixedDims<A, K, true>
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -127,6 +128,7 @@ struct Model {
                              // gather of J' f instead of the scatter (FM_NO_SCATTER=1); bit 7 = the serial arm
                              // kinematics (FM_SERIAL_FK=1); bit 8 = the Newton warmstart's two row passes
                              // (FM_TWO_PASS_SETUP=1)
+  int ovf_abort;             // 1: a stage above the contact capacity abandons the env-step (State::rerun), not cut it
 };
 
 template <typename T>
@@ -143,6 +145,12 @@ struct State {
   // DimsSpill: per-arena global scratch blocks (Lay::gtotal bytes each) for the Hessian and the contact records
   gptr<char> spill{nullptr};
   long long spill_stride{0};
+  // (2,4) contact overflow: [0] = count, [1 + i] = arena ids whose env-step the 64-contact kernel abandoned (its
+  // record untouched) for the wide rerun kernel.  Null: the capacity cut (counted in counters[0]) instead
+  gptr<int32_t> rerun{nullptr};
+  // IK classes with `rerun`: the arena's task records (dbl, ints) as the env-step found them, restored by the rerun
+  // (the IK compose writes the FSM and the toggles' last actions before the substeps)
+  gptr<char> bak{nullptr};
 };
 
 // the arena's global scratch block (nullptr unless the kernel runs a DimsSpill layout)
@@ -274,7 +282,7 @@ enum { PH_FK = 0, PH_GEOM, PH_COLL, PH_ROWS, PH_SMOOTH, PH_NSETUP, PH_NGRAD, PH_
        PH_NFINAL, PH_INT, PH_TAIL, PH_NCON, PH_KHZ, PH_CBOUND, PH_CMID, PH_CNARROW, PH_CHDIAG, PH_CHPANEL, PH_CHTRAIL,
        PH_CHSOLVE, PH_LAST = 23, FM_NPROF = 24 };
 enum { MISC_NCON = 0, MISC_NROW, MISC_NSURV, MISC_DROP, MISC_ITER, MISC_MAXIT, MISC_FLAG, MISC_NSTAGE, MISC_CSUM,
-       MISC_CMAX, MISC_MC_OK, MISC_MC_N, MISC_MC_TOT };
+       MISC_CMAX, MISC_MC_OK, MISC_MC_N, MISC_MC_TOT, MISC_OVF };
 // cached midphase (scenes with DIM::midcache): the body-pair hit list of an inflated bounding test is reused across
 // substeps until a moving collision body has travelled MC_HALF from where it was when the list was built
 // hit pairs a cached list holds (more: no caching that substep); the (2,4) scene has LDS room for 40 within its
@@ -287,8 +295,8 @@ constexpr double MC_MARGIN = FM_MC_MARGIN;    // m added to every bound (sphere 
 constexpr double MC_HALF = 0.5 * MC_MARGIN;  // rebuild once any moving body has moved this far (both ends: MC_MARGIN)
 // per-arena int64 counters (fm_get_counters): contacts dropped for capacity, Newton iterations, Newton
 // max-iteration hits, bucket-index anomalies, contacts summed over stages, max contacts in one stage,
-// objects in scene summed over env-steps, episodes ended
-constexpr int FM_NCTR = 8;
+// objects in scene summed over env-steps, episodes ended, env-steps rerun at the wide contact capacity
+constexpr int FM_NCTR = 9;
 // packed geom info
 enum { GC_PLANE = 0, GC_SPHERE = 1, GC_BOX = 2, GI_ARM = 2, GI_PC = 3 };
 
@@ -585,15 +593,21 @@ struct DimsSpill : Dims {
   __host__ __device__ DimsSpill(const Dims& d) : Dims(d) {}
 };
 
-template <int A_, int K_>
+// WIDE_: the benchmark scene's rerun kernel -- the (2,4) scene at the wide contact capacity, stepping the arenas whose
+// env-step the 64-contact kernel abandoned at a stage with more contacts (State::rerun), so no contact is dropped
+#ifndef FM_SPILL24
+#define FM_SPILL24 0  // experiment builds: the (2,4) kernel's Hessian + contact records in global scratch (occupancy A/B)
+#endif
+template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
-  static constexpr bool spill = false;
+  static constexpr bool spill = FM_SPILL24 && A_ == 2 && K_ == 4 && !WIDE_;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
   static constexpr bool midcache = true;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;
-  static constexpr int MAXC = (A_ == 2 && K_ == 4) ? MAXCON : MAXCON_WIDE;
+  static constexpr int MAXC = (A_ == 2 && K_ == 4 && !WIDE_) ? MAXCON : MAXCON_WIDE;
+  static constexpr bool rerun = WIDE_;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
@@ -602,7 +616,7 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, false, midcache, MAXC == WAVE);
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

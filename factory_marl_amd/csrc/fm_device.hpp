@@ -395,7 +395,7 @@ struct Ws {
   __device__ __forceinline__ T* H() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.H);
+      return (T*)((DIM::spill ? gbase : base) + c.H);
     } else if constexpr (DIM::spill) {
       return (T*)(gbase + L->H);
     } else {
@@ -413,7 +413,7 @@ struct Ws {
   __device__ __forceinline__ T* cr() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.c_r);
+      return (T*)((DIM::spill ? gbase : base) + c.c_r);
     } else if constexpr (DIM::spill) {
       return (T*)(gbase + L->c_r);
     } else {
@@ -1564,7 +1564,12 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // 5. sort the staged contacts by key into the contact slots
   const int nst = misc[MISC_NSTAGE];
   const int ncon = nst < dm.maxcon ? nst : dm.maxcon;
-  if (LANE == 0 && nst > dm.maxcon) ctr[0] += nst - dm.maxcon;
+  // above capacity: the excess is counted as dropped, unless the env-step will be abandoned and rerun at the wide
+  // capacity (the benchmark scene, M.ovf_abort; the kernel reads MISC_OVF after the stage)
+  if (LANE == 0) {
+    misc[MISC_OVF] = nst > dm.maxcon ? nst - dm.maxcon : 0;
+    if (nst > dm.maxcon && !M.ovf_abort) ctr[0] += nst - dm.maxcon;
+  }
   // rank of each staged contact among the staged keys: contacts c = LANE + 64 h (h < DIM::MAXC / 64), the keys
   // broadcast by v_readlane
   constexpr int NHC = DIM::MAXC / WAVE;
@@ -3939,13 +3944,16 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& 
 // gather_JtF by scatter ((2,4) scene): one lane per (contact, Jacobian column) adds its column's product with the
 // contact's frame force into a float64 accumulator by LDS atomics (one wave: a fixed order), one lane per generic
 // row likewise; the per-dof loop above is a chain of dependent LDS reads on the belt's lane, which carries every
-// belt contact.  acc: nv doubles of scratch (the solver's tmp, dead at the gradient and at the final forces).
+// belt contact.  The belt's column (dof 0, in every belt contact) is summed in registers and reduced by one wave
+// sum: same-address float64 atomics of all belt contacts serialise in the LDS.  acc: nv doubles of scratch (the
+// solver's tmp, dead at the gradient and at the final forces).
 template <typename T, typename DIM, typename O>
 __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, O* out,
                                               double* acc) {
   const DIM dm(M.dm);
   for (int i = LANE; i < dm.nv; i += WAVE) acc[i] = 0.0;
   SYNC();
+  double vb = 0.0;
   for (int e = LANE; e < CJ * ncon; e += WAVE) {
     const int c = e / CJ, ii = e - CJ * c;
     const int* ci = w.ci() + 4 * c;
@@ -3955,8 +3963,15 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
     const double* f3 = dslot(cr, CR_F3);
     const double v = (double)J[ii] * f3[0] + (double)J[CJ + ii] * f3[1] + (double)J[2 * CJ + ii] * f3[2];
     const int gi = ii < nda ? tree_dof(dm, ta) + ii : tree_dof(dm, tb >= 0 ? tb : 0) + ii - nda;
-    if (ii < nda + ndb) atomicAdd(acc + gi, v);
+    if (ii < nda + ndb) {
+      if (gi == 0)
+        vb += v;
+      else
+        atomicAdd(acc + gi, v);
+    }
   }
+  vb = wave_sum(vb);
+  if (LANE == 0) acc[0] += vb;  // generic rows never act on the belt dof
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
     const T* rr = w.rr() + RR_N * r;
@@ -5017,8 +5032,16 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
 
 // IK: the env class may compose IK proposals (every class but AllFullRL); the AllFullRL instantiation carries
 // none of the IK code (and none of its register demand)
+#ifndef FM_WAVES_PER_EU
+#define FM_WAVES_PER_EU 0  // experiment builds: the minimum waves per SIMD the register allocation must allow
+#endif
+#if FM_WAVES_PER_EU > 0
+#define FM_STEP_ATTR __attribute__((amdgpu_waves_per_eu(FM_WAVES_PER_EU)))
+#else
+#define FM_STEP_ATTR
+#endif
 template <typename T, typename DIM, bool IK>
-__global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
+__global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> params) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   (void)params;
   // All launch parameters are read through an opaque pointer to the kernarg segment at each use, so the
@@ -5031,11 +5054,23 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   // longest-processing-time-first dispatch: the host orders the arenas by their last env-step's duration, so the
   // expensive ones start in the first wave of workgroups and the cheap ones fill the tail (results do not depend
   // on which workgroup steps an arena)
-  const int32_t* const order_ = S.order;
-  const int arena = order_ ? order_[blockIdx.x] : (int)blockIdx.x;
+  int arena_sel;
+  if constexpr (DIM::rerun) {
+    // the wide-capacity rerun: workgroup b steps the b-th arena the 64-contact launch abandoned (none: exit)
+    const int32_t* const rr = S.rerun;
+    if ((int)blockIdx.x >= rr[0]) return;
+    arena_sel = rr[1 + blockIdx.x];
+  } else {
+    const int32_t* const order_ = S.order;
+    arena_sel = order_ ? order_[blockIdx.x] : (int)blockIdx.x;
+  }
+  const int arena = arena_sel;
   const unsigned long long t_begin = wall_clock64();
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K, nu = dm.nu;
+  // abandon the env-step at a stage above the contact capacity (benchmark scene with a rerun list): the arena's
+  // records stay as the step found them and the wide kernel (FixedDims<2, 4, true>) steps it again after this launch
+  constexpr bool can_abandon = DIM::fixed && !DIM::rerun && DIM::MAXC == WAVE;
   // a fresh opaque LDS base per use: workspace addresses are recomputed inside each phase instead of
   // being hoisted out of the substep loop (which would keep every phase's addresses live everywhere)
 #define w (Ws<T, DIM>{lds_base(smem), &L, spill_base<DIM>(S, arena)})
@@ -5050,6 +5085,32 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
 #define rng (S.rng + 4 * (size_t)arena)
 #define ctr (S.counters + FM_NCTR * (size_t)arena)
 #define act (io.actions + (size_t)arena * dm.act_dim)
+  if constexpr (IK && (can_abandon || DIM::rerun)) {
+    // the IK compose below writes the FSM / last-action blocks of the task records: keep the step's starting
+    // records for a rerun (the rerun restores them first)
+    char* const bk = S.bak;
+    if (bk) {
+      double* bd = (double*)(bk + (size_t)arena * (8 * dm.dbl_stride + 4 * dm.int_stride));
+      int32_t* bi = (int32_t*)(bd + dm.dbl_stride);
+      double* dd = S.dbl + (size_t)arena * dm.dbl_stride;
+      for (int i = LANE; i < dm.dbl_stride; i += WAVE) {
+        if (DIM::rerun)
+          dd[i] = bd[i];
+        else
+          bd[i] = dd[i];
+      }
+      for (int i = LANE; i < dm.int_stride; i += WAVE) {
+        if (DIM::rerun)
+          ti[i] = bi[i];
+        else
+          bi[i] = ti[i];
+      }
+      FULL_SYNC();
+    }
+  }
+  if constexpr (DIM::rerun) {
+    if (LANE == 0) ctr[8] += 1;
+  }
   // ---- ctrl_target (double) and the env class's control (environments.py _compose_control, base_env.py:255-262)
 #define ctrl_ (w.ctrl())
   const double* dsrc = S.dbl + (size_t)arena * dm.dbl_stride;
@@ -5118,6 +5179,20 @@ __global__ void __launch_bounds__(64) step_kernel(StepParams<T> params) {
   //   then the task layer; on termination one more pass = reset_sim's forward (stage, smooth, solve).
   for (int t = 0;; t++) {
     stage(M, w, arena, ctr);
+    if constexpr (can_abandon) {
+      // uniform (LDS scalar); experiment switch 512 (FM_FORCE_RERUN=1): every env-step goes to the wide kernel
+      if (S.rerun && (w.misc()[MISC_OVF] > 0 || (M.dbg_flags & 512))) {
+        if (!reset_pass) {
+          if (LANE == 0) {
+            int32_t* const rr = S.rerun;
+            rr[1 + atomicAdd(rr, 1)] = arena;
+          }
+          return;
+        }
+        // the reset pass's forward (after the task layer wrote the records) cannot be abandoned: cut and count
+        if (LANE == 0) ctr[0] += w.misc()[MISC_OVF];
+      }
+    }
     if (t == 0 && !reset_pass) {
       load_state(M, S, w, arena, false);
       SYNC();

@@ -1,8 +1,12 @@
 // fm_fixed.hip -- one compile-time scene (FM_A arms, FM_K objects): instantiates the env-step kernel
 // with FixedDims<FM_A, FM_K> (constexpr dims and LDS layout) for one precision (FM_PREC 32 or 64).  Built
 // once per scene and precision by the Makefile (fm_fixed_<A>_<K>_f<P>.o) so they compile in parallel.
+// FM_WIDE=1: the same scene's wide-capacity rerun kernel instead (fm_rerun_f<P>.o, the benchmark scene).
 #include "fm_device.hpp"
 
+#ifndef FM_WIDE
+#define FM_WIDE 0
+#endif
 #ifndef FM_A
 #error "compile with -DFM_A=<arms> -DFM_K=<objects> -DFM_PREC=<32|64>"
 #endif
@@ -39,7 +43,41 @@ void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStre
     hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>, false>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
 }
 
+#if FM_WIDE
+// the benchmark scene's wide-capacity rerun (FixedDims<A, K, true>): workgroup b steps arena S.rerun[1 + b] when
+// b < S.rerun[0]; launched with one workgroup per arena of the handle, so every abandoned arena has its workgroup
+template <typename T, int A, int K>
+hipError_t rerun_set_attr() {
+  const int lds = FixedDims<A, K, true>::template layout<sizeof(T)>().total;
+  hipError_t e = hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K, true>, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K, true>, true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+template <typename T, int A, int K>
+Lay rerun_layout() {
+  return FixedDims<A, K, true>::template layout<sizeof(T)>();
+}
+
+template <typename T, int A, int K>
+void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik) {
+  const int lds = FixedDims<A, K, true>::template layout<sizeof(T)>().total;
+  if (ik)
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, true>), dim3(num_arenas), dim3(WAVE), lds, stream, p);
+  else
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, false>), dim3(num_arenas), dim3(WAVE), lds, stream, p);
+}
+
+static_assert(FixedDims<FM_A, FM_K, true>::template layout<sizeof(FM_REAL)>().total <= 160 * 1024,
+              "wide rerun workspace exceeds the CU's LDS");
+template hipError_t rerun_set_attr<FM_REAL, FM_A, FM_K>();
+template Lay rerun_layout<FM_REAL, FM_A, FM_K>();
+template void rerun_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, hipStream_t, bool);
+#else
 template hipError_t fixed_set_attr<FM_REAL, FM_A, FM_K>(int);
 template void fixed_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, int, hipStream_t, bool);
+#endif
 
 }  // namespace fm

@@ -41,7 +41,8 @@ TOGGLE_CLASSES = envs.TOGGLE_CLASSES
 # the kernel's experiment switches (fm_api.hip read_experiment_flags): (environment variable, value) -> flag bit
 EXPERIMENT_FLAGS = {("FM_CHOL_LDS", "1"): 1, ("FM_CHOL_LDS", "2"): 2, ("FM_SERIAL_BOXBOX", "1"): 4,
                     ("FM_NO_MIDCACHE", "1"): 8, ("FM_NO_ARROW", "1"): 16, ("FM_NO_ARROW", "2"): 32,
-                    ("FM_NO_SCATTER", "1"): 64, ("FM_SERIAL_FK", "1"): 128, ("FM_TWO_PASS_SETUP", "1"): 256}
+                    ("FM_NO_SCATTER", "1"): 64, ("FM_SERIAL_FK", "1"): 128, ("FM_TWO_PASS_SETUP", "1"): 256,
+                    ("FM_FORCE_RERUN", "1"): 512, ("FM_NO_RERUN", "1"): 1024}
 
 # global scalars of the handle (fm_set_param), per-arena values of the state record, fixed at creation
 RUNTIME_PARAMS = ("pt_time", "initial_conveyor_speed", "conveyor_acceleration", "force_contact_threshold",
@@ -470,7 +471,7 @@ class FactoryVecEnv:
 
     def counters(self):
         self._bind_stream()
-        out = np.zeros((self.num_envs, 8), np.int64)
+        out = np.zeros((self.num_envs, _lib.num_counters(self._L)), np.int64)
         _lib.check(self._L.fm_get_counters(self._h, out.ctypes.data_as(C.c_void_p)))
         return out
 

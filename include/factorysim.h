@@ -146,12 +146,15 @@ int fm_state_size(const fm_handle* h);                 /* bytes per arena of the
 int fm_get_state(fm_handle* h, void* host_out);        /* [N * fm_state_size] */
 int fm_set_state(fm_handle* h, const void* host_in);
 
-/* Diagnostics: per-arena counters accumulated since create (host [N*8] int64):
+/* Diagnostics: per-arena counters accumulated since create (host [N * fm_num_counters()] int64):
  * [0] contacts dropped for capacity, [1] Newton iterations, [2] solver max-iteration hits,
  * [3] bucket-index anomalies (task_utils.py:103-113 would raise IndexError),
  * [4] contacts summed over physics stages, [5] most contacts in one stage (both before any capacity
- * cut), [6] objects in scene summed over env-steps, [7] episodes ended (terminations). */
+ * cut), [6] objects in scene summed over env-steps, [7] episodes ended (terminations),
+ * [8] env-steps rerun by the (2,4) scene's wide-capacity kernel (a stage above 64 contacts; the Newton counters
+ * [1] [2] then include the abandoned part of the step). */
 int fm_get_counters(fm_handle* h, int64_t* host_out);
+int fm_num_counters(void);
 
 /* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [24] uint64).
  * mode 1 = zero and enable, 0 = disable, -1 = leave as is; host_out (may be NULL) receives the

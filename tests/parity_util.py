@@ -5,7 +5,9 @@ each env-step (physics stage + task layer, exported in the product's record layo
 GPU arena each, every arena is stepped once with the action the oracle used, and the GPU's resulting
 state / obs / reward / flags are compared with the oracle's step.
 Metric: |dq| / max(|ref|, 1) and |dv| / max(|ref|, 0.1), the max over the arena's
-qpos / qvel; integer task state, RNG, scores, num_obj and done flags compared bit for bit.
+qpos / qvel; integer task state, RNG, scores, num_obj and done flags compared bit for bit.  On a terminating
+step the GPU's record after the step is the auto-reset one: it is compared with the oracle's record after
+e.reset() (integers / RNG exact, the float record and reset()'s observation within a tolerance).
 """
 import numpy as np
 
@@ -37,7 +39,11 @@ def rollout(oracle, A, K, T, reward="progress", seed_actions=7, amp=2.0, weights
         outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
         acts.append(a)
         if term:
-            e.reset()
+            # SB3 auto-reset: the record the next env-step starts from (TaskManager RNG continuing, counters and
+            # memories reset) and reset()'s observation -- what the GPU's record / obs hold after a terminating step
+            robs = e.reset()
+            rd, ri, rr = e.export_state()
+            outs[-1]["reset"] = dict(obs=robs, dbl=rd, ints=ri, rng=rr)
     return np.stack(recs), np.stack(acts), outs
 
 
@@ -60,6 +66,10 @@ def restep_at_tolerance(oracle, A, K, trajectory, tol, env_class="AllFullRLProgr
             L.or_set_solver_tol(0.0)
             d2, i2, r2 = p.export_state()
             outs.append(dict(obs=obs, reward=rew, term=term, info=info, dbl=d2, ints=i2, rng=r2))
+            if term:
+                robs = p.reset()
+                rd, ri, rr = p.export_state()
+                outs[-1]["reset"] = dict(obs=robs, dbl=rd, ints=ri, rng=rr)
     finally:
         L.or_set_solver_tol(0.0)
     return recs, acts, outs
@@ -114,7 +124,10 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
 
     recs, acts, outs = trajectory
     n = len(recs)
+    experiment = kw.pop("experiment", "")
     env = gpu_env(n, precision, A, K, env_class, **kw)
+    if experiment:
+        env.set_experiment(experiment)  # kernel experiment switches (FactoryVecEnv.set_experiment)
     env.set_state(recs)
     obs, rew, term, _ = env.step_tensors(torch.as_tensor(acts, device=env.device))
     env.sync()
@@ -123,6 +136,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     tobs = env.terminal_obs.cpu().numpy()
     nq = 1 + 7 * K + 9 * A
     errs, err_steps, int_bad, flag_bad, obs_err, rew_err, ik_err = [], [], [], [], [], [], []
+    reset_bad, reset_err = [], []
     for s in range(n):
         o = outs[s]
         if bool(term[s]) != o["term"]:
@@ -130,6 +144,14 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
             continue
         if o["term"]:
             obs_err.append(np.abs(tobs[s] - o["obs"]).max())
+            if "reset" in o:
+                # the post-auto-reset record: integers / RNG exact, state and warmstart and reset obs close
+                rs = o["reset"]
+                gd, gi, gr = st.unpack(A, K, got[s])
+                if not (np.array_equal(gi, rs["ints"]) and np.array_equal(gr, rs["rng"])):
+                    reset_bad.append(s)
+                reset_err.append(max(float((np.abs(gd - rs["dbl"]) / np.maximum(np.abs(rs["dbl"]), 1.0)).max()),
+                                     float(np.abs(obs[s] - rs["obs"]).max())))
             continue
         gd, gi, gr = st.unpack(A, K, got[s])
         # every integer of the record: TaskManager lists / counters / scores, the episode length (Monitor "l") and
@@ -150,6 +172,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     cnt = env.counters()
     env.close()
     return dict(errs=np.array(errs), err_steps=np.array(err_steps, int), int_bad=int_bad, flag_bad=flag_bad,
+                reset_bad=reset_bad, reset_err=np.array(reset_err), resets=len(reset_err),
                 obs_err=np.array(obs_err), rew_err=np.array(rew_err), counters=cnt, ik_err=np.array(ik_err),
                 terms=int(sum(o["term"] for o in outs)), max_cubes=max(o["info"]["num_obj"] for o in outs))
 
@@ -163,4 +186,6 @@ def summary(r, gate=1e-4):
                 contacts_dropped=int(r["counters"][:, 0].sum()), terminations=r["terms"], max_cubes=r["max_cubes"],
                 newton_iters_per_substep=round(float(r["counters"][:, 1].sum()) / (100.0 * len(r["counters"])), 3),
                 newton_maxit_hits=int(r["counters"][:, 2].sum()),
-                missing_steps=[int(s) for s in r["err_steps"][e > gate]])
+                missing_steps=[int(s) for s in r["err_steps"][e > gate]],
+                resets_compared=r.get("resets", 0), reset_bad=len(r.get("reset_bad", [])),
+                reset_worst=float(r["reset_err"].max()) if r.get("resets", 0) else 0.0)

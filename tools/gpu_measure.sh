@@ -6,12 +6,14 @@
 #   LIB=path        library for the steps (FACTORYSIM_LIB; default factory_marl_amd/libfactorysim.so)
 #   SWEEP="specs"   parity-sweep trajectories (A,K,T,seed[,EnvClass[,oracle_tol]]; default: the four long ones)
 #   SFX=name        suffix for the output files of the steps (A/B runs of two libraries in one TAG)
+#   TOL=x           Newton tolerance of the sweeps' GPU env (0 = the precision's default)
 # steps:
 #   tests       pytest -m gpu (verbose, prints kept)          sweep32 / sweep64   parity sweep fp32 / fp64
 #   bench       default bench line (with the CPU baseline)    quick               bench, 30 steps, no CPU leg
 #   c3 c4 c5    config 3 / 4 (one GPU) / 5 benches             ktrace              rocprofv3 kernel trace + stats
 #   pmc         PMC passes (FETCH, WRITE, SQ, VALU) + summaries
-#   phase       phase profiles (2,4) fp32 / fp64, (2,8), (4,16)
+#   phase       phase profiles (2,4) fp32 / fp64, (2,8), (4,16)     phase24   (2,4) fp32 only
+#   pmcsq       the SQ counter pass alone (waits, LDS bank conflicts)
 #   flags       1000-episode flag-divergence study (fp32, fp64)
 set -o pipefail
 TAG=${1:?tag}
@@ -31,18 +33,18 @@ for step in "$@"; do
   echo "== $step$S $(date +%T)"
   case $step in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -v -s -x --timeout 300 --timeout-method thread > $O/tests$S.log 2>&1 \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $O/tests$S.log 2>&1 \
         || fail tests $? $O/tests$S.log
       tail -2 $O/tests$S.log ;;
     sweep32|sweep64)
       pr=fp${step#sweep}
-      timeout -k 10 600 python -u tools/parity_sweep.py --prec $pr --tag $step$S --verbose-tol 1e-4 --traj $SWEEP \
+      timeout -k 10 600 python -u tools/parity_sweep.py --prec $pr --tag $step$S --verbose-tol 1e-4 --tol ${TOL:-0} --traj $SWEEP \
         > $O/$step$S.log 2> $O/$step$S.err || fail $step $? $O/$step$S.err
       grep '^{' $O/$step$S.log > $O/$step$S.jsonl
       python -c "
 import json
 for l in open('$O/$step$S.jsonl'):
-    r = json.loads(l); print(r['prec'], r['traj'], r['within'], '%.3e' % r['worst'], r['int_bad'], r['flag_bad'], r['missing_steps'][:10])
+    r = json.loads(l); print(r['prec'], r['traj'], r['within'], '%.3e' % r['worst'], r['int_bad'], r['flag_bad'], r['missing_steps'][:10], 'resets', r['resets_compared'], r['reset_bad'], '%.1e' % r['reset_worst'])
 " ;;
     bench)
       timeout -k 10 400 python bench.py > $O/bench$S.json 2> $O/bench$S.err || fail bench $? $O/bench$S.err
@@ -85,6 +87,15 @@ for l in open('$O/$step$S.jsonl'):
       python tools/pmc_traffic.py $F $W --arenas 4096 --out $O/pmc_traffic$S.json || fail traffic $?
       python tools/pmc_valu.py $V --arenas 4096 --last 3 --out $O/pmc_valu$S.json || fail valu $?
       python tools/pmc_sq.py $Q $O/pmc_sq_summary$S.json || fail sq $? ;;
+    phase24)
+      timeout -k 10 200 python tools/phase_profile.py --precision fp32 > $O/phase_fp32$S.json 2> $O/phase$S.err \
+        || fail phase24 $? $O/phase$S.err ;;
+    pmcsq)
+      timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+        SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $O/pmc_sq$S -- python3 bench.py $P \
+        > $O/pmc_sq$S.log 2>&1 || fail pmc_sq $? $O/pmc_sq$S.log
+      python tools/pmc_sq.py $(find $O/pmc_sq$S -name "*counter_collection.csv" | head -1) $O/pmc_sq_summary$S.json \
+        || fail sq $? ;;
     phase)
       timeout -k 10 200 python tools/phase_profile.py --precision fp32 > $O/phase_fp32$S.json 2> $O/phase$S.err \
         || fail phase32 $? $O/phase$S.err

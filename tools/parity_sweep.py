@@ -44,6 +44,8 @@ def load_traj(A, K, T, seed, env_class="AllFullRLProgressRewardEnv",
         for s in range(T):
             outs.append(dict(obs=z["obs"][s], reward=float(z["reward"][s]), term=bool(z["term"][s]),
                              info=meta["info"][s], dbl=z["dbl"][s], ints=z["ints"][s], rng=z["rng"][s]))
+            if outs[-1]["term"] and "reset_dbl" in z:
+                outs[-1]["reset"] = {k: z["reset_" + k][s] for k in ("obs", "dbl", "ints", "rng")}
         return z["recs"], z["acts"], outs
     recs, acts, outs = pu.rollout(po, A, K, T, seed_actions=seed, env_class=env_class)
     _save(f, recs, acts, outs)
@@ -51,10 +53,17 @@ def load_traj(A, K, T, seed, env_class="AllFullRLProgressRewardEnv",
 
 
 def _save(f, recs, acts, outs):
+    extra = {}
+    rs = [o.get("reset") for o in outs]
+    if any(r is not None for r in rs):
+        # the oracle's post-auto-reset record of terminating steps (zeros elsewhere)
+        r0 = next(r for r in rs if r is not None)
+        for k in ("obs", "dbl", "ints", "rng"):
+            extra["reset_" + k] = np.stack([r[k] if r is not None else np.zeros_like(r0[k]) for r in rs])
     np.savez(f, recs=recs, acts=acts, obs=np.stack([o["obs"] for o in outs]),
              reward=np.array([o["reward"] for o in outs]), term=np.array([o["term"] for o in outs]),
              dbl=np.stack([o["dbl"] for o in outs]), ints=np.stack([o["ints"] for o in outs]),
-             rng=np.stack([o["rng"] for o in outs]))
+             rng=np.stack([o["rng"] for o in outs]), **extra)
     json.dump(dict(info=[o["info"] for o in outs]), open(f[:-4] + ".json", "w"))
 
 
