@@ -572,6 +572,7 @@ static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik) {
   pr.S.order = nullptr;
   pr.S.rerun = h->rerun;
   pr.S.bak = h->bak;
+  pr.M.dm.maxcon = MAXCON_WIDE;  // the wide kernel keeps up to 128 contacts per stage
   rerun_launch<T, 2, 4>(pr, h->dm.N, h->stream, ik);
 }
 

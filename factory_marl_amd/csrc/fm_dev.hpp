@@ -575,7 +575,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   if (spill) {  // the two largest arrays in the arena's global scratch block (L2 / HBM) instead of LDS
     L.spill = 1;
     L.H = 0;
-    L.c_r = (tsize * nv * nv + 15) & ~15;
+    L.c_r = (tsize * (hstride(tsize, nv) * hstride(tsize, nv) + hextra(tsize, nv)) + 15) & ~15;
     L.gtotal = L.c_r + ((tsize * CR_N * maxcon + 255) & ~255);
   }
   return L;
@@ -598,10 +598,13 @@ struct DimsSpill : Dims {
 #ifndef FM_SPILL24
 #define FM_SPILL24 0  // experiment builds: the (2,4) kernel's Hessian + contact records in global scratch (occupancy A/B)
 #endif
+#ifndef FM_SPILL416
+#define FM_SPILL416 0  // experiment builds: the same for the fp32 (4,16) kernel (155.9 KB of LDS: one arena per CU)
+#endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
-  static constexpr bool spill = FM_SPILL24 && A_ == 2 && K_ == 4 && !WIDE_;
+  static constexpr bool spill = (FM_SPILL24 && A_ == 2 && K_ == 4 && !WIDE_) || (FM_SPILL416 && A_ == 4 && K_ == 16);
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
   static constexpr bool midcache = true;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;

@@ -1131,9 +1131,13 @@ __device__ __forceinline__ void narrow_batch(const Model<T>& M, const Ws<T, DIM>
     const int kb1 = (gi1 >> 8) & 255, kb2 = (gi2 >> 8) & 255;
     const int lo = c1 < c2 ? c1 : c2, hi = c1 < c2 ? c2 : c1;
     Emit<T> emit{w.stage(), w.skey(), w.spw(), w.misc() + MISC_NSTAGE, dm.maxcon, (lo << 15) | (hi << 3), pwd, 0};
-    set_anchor(w, dm, kb1, kb2, emit);
     double p1[3], R1[9], h1[3], p2[3], R2[9], h2[3];
     geom_pose_f64(M, w, c2, kb2, p2, R2, h2);
+    const int ak = anchor_cube(dm, kb1, kb2);
+    // the anchor (contact_anchor) is the cube's centre, i.e. its geom's pose
+    if (ak < 0 || ak != kb2 - 2) contact_anchor(w, ak, emit.o);
+    else
+      for (int k = 0; k < 3; k++) emit.o[k] = p2[k];
     if (t1 == GC_PLANE) {
       if (t2 == GC_SPHERE)
         np_plane_sphere(p2, M.geomd[16 * c2 + 15], emit, zshift<T>());
@@ -2191,9 +2195,13 @@ __device__ __forceinline__ void arm_jac_col(const Ws<T, DIM>& w, int arm, int b,
 // cube itself); an arm body's point in the kernel frame
 template <typename T, typename DIM>
 __device__ __forceinline__ void body_jac_point(const Model<T>& M, const Ws<T, DIM>& w, int kb, const T* p,
-                                               const double* o, T* pt) {
+                                               const double* o, int ak, T* pt) {
   const DIM dm(M.dm);
-  if (kb >= 2 && kb < 2 + dm.K) {
+  if (kb - 2 == ak) {  // the anchor cube itself: the stored point is its lever arm
+    pt[0] = p[0];
+    pt[1] = p[1];
+    pt[2] = p[2];
+  } else if (kb >= 2 && kb < 2 + dm.K) {
     const double* c = w.qd() + 1 + 7 * (kb - 2);
     pt[0] = p[0] + (T)(o[0] - c[0]);
     pt[1] = p[1] + (T)(o[1] - c[1]);
@@ -2372,7 +2380,9 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   PMARK(PH_COLL);
   const int ncon = misc[MISC_NCON];
   if (M.prof && LANE == 0) w.prof()[PH_NCON] += ncon;
-  // ---- contact rows: frame, Jacobian blocks, impedance, D, reference-acceleration terms
+  // ---- contact rows: frame, Jacobian blocks, impedance, D, reference-acceleration terms (one lane per contact;
+  // round 4 measured one lane per (contact, column) slower: rows 5.3 -> 7.5 us per arena-substep, the frame and
+  // point reloads of every column outweigh the shorter chain)
   for (int c = LANE; c < ncon; c += WAVE) {
     int* ci = w.ci() + 4 * c;
     T* cr = w.cr() + CR_N * c;
@@ -2437,10 +2447,11 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     int ndb = tb >= 0 ? tree_nd(dm, tb) : 0;
     const T p[3] = {cr[CR_POS], cr[CR_POS + 1], cr[CR_POS + 2]};
     double o[3];
-    contact_anchor(w, anchor_cube(dm, kb1, kb2), o);
+    const int ak = anchor_cube(dm, kb1, kb2);
+    contact_anchor(w, ak, o);
     T pt1[3], pt2[3];
-    body_jac_point(M, w, kb1, p, o, pt1);
-    body_jac_point(M, w, kb2, p, o, pt2);
+    body_jac_point(M, w, kb1, p, o, ak, pt1);
+    body_jac_point(M, w, kb2, p, o, ak, pt2);
     T* J = cr + CR_J;
     for (int blk = 0; blk < 2; blk++) {
       int t = blk == 0 ? ta : tb;
@@ -3944,16 +3955,15 @@ __device__ __forceinline__ void gather_JtF(const Model<T>& M, const Ws<T, DIM>& 
 // gather_JtF by scatter ((2,4) scene): one lane per (contact, Jacobian column) adds its column's product with the
 // contact's frame force into a float64 accumulator by LDS atomics (one wave: a fixed order), one lane per generic
 // row likewise; the per-dof loop above is a chain of dependent LDS reads on the belt's lane, which carries every
-// belt contact.  The belt's column (dof 0, in every belt contact) is summed in registers and reduced by one wave
-// sum: same-address float64 atomics of all belt contacts serialise in the LDS.  acc: nv doubles of scratch (the
-// solver's tmp, dead at the gradient and at the final forces).
+// belt contact.  (Round 4: reducing the belt's column by a wave sum instead of its same-address atomics was measured
+// slower -- gradient 5.22 -> 5.70 us per arena-substep -- and left the LDS bank-conflict rate unchanged.)  acc: nv
+// doubles of scratch (the solver's tmp, dead at the gradient and at the final forces).
 template <typename T, typename DIM, typename O>
 __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, O* out,
                                               double* acc) {
   const DIM dm(M.dm);
   for (int i = LANE; i < dm.nv; i += WAVE) acc[i] = 0.0;
   SYNC();
-  double vb = 0.0;
   for (int e = LANE; e < CJ * ncon; e += WAVE) {
     const int c = e / CJ, ii = e - CJ * c;
     const int* ci = w.ci() + 4 * c;
@@ -3963,15 +3973,8 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
     const double* f3 = dslot(cr, CR_F3);
     const double v = (double)J[ii] * f3[0] + (double)J[CJ + ii] * f3[1] + (double)J[2 * CJ + ii] * f3[2];
     const int gi = ii < nda ? tree_dof(dm, ta) + ii : tree_dof(dm, tb >= 0 ? tb : 0) + ii - nda;
-    if (ii < nda + ndb) {
-      if (gi == 0)
-        vb += v;
-      else
-        atomicAdd(acc + gi, v);
-    }
+    if (ii < nda + ndb) atomicAdd(acc + gi, v);
   }
-  vb = wave_sum(vb);
-  if (LANE == 0) acc[0] += vb;  // generic rows never act on the belt dof
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
     const T* rr = w.rr() + RR_N * r;

@@ -298,6 +298,8 @@ void or_env_set_timing(or_env* e, double pt_time, double control_frequency) {
   e->t.frame_skip = (int)((1.0 / control_frequency) / 0.001);
 }
 int or_env_ik_steps(const or_env* e) { return e->ik_steps; }
+long or_env_ik_calls(const or_env* e, int arm) { return e->ik_calls[arm]; }
+long or_env_ik_fails(const or_env* e, int arm) { return e->ik_fails[arm]; }
 void or_env_ik_arm(const or_env* e, int i, int* ai, double* ad) { arm_to_flat(&e->ik[i], ai, ad); }
 
 /* golden replay of FactoryManipulationEnv._compose_control with the reference's (fake) IK results in call

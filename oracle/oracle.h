@@ -120,6 +120,7 @@ void or_make_constraint(const or_model* m, or_data* d);
 void or_step1(const or_model* m, or_data* d);
 void or_step2(const or_model* m, or_data* d);
 void or_set_accel_noise(double amp, uint64_t seed); /* sensitivity probe only (tools/fp32_floor.py) */
+void or_set_probe(int mask, double amp, uint64_t seed); /* data-precision probe only (tools/fp32_floor.py) */
 void or_set_solver_tol(double tol);                /* Newton tolerance study only (tools/tolerance_floor.py) */
 void or_forward(const or_model* m, or_data* d); /* step1 + acceleration stage, no integration */
 void or_jac_point(const or_model* m, const or_data* d, int body, const double p[3], double* jacp, double* jacr);
@@ -217,6 +218,8 @@ typedef struct or_env {
   double pause_last[OR_IK_MAXA][8]; /* PauseIKToggleEnv.last_arm_actions */
   or_data* ik_d;                    /* scratch physics copy of qpos_from_site_pose (inplace=False) */
   int ik_steps;                     /* diagnostics: IK iterations summed over the last compose */
+  long ik_calls[OR_IK_MAXA];        /* diagnostics (tools/base_policy_study.py): IK solves per arm since creation, */
+  long ik_fails[OR_IK_MAXA];        /* and the ones that did not converge (act() returns last_ctrl) */
   double* stage_qpos; /* state at which the current position/velocity stage was computed (last mj_step1) */
   double* stage_qvel;
   double ep_return;

@@ -98,6 +98,7 @@ def _bind(L, real):
             "or_env_import": (None, [P, P, P, P]),
             "or_batch_bench": (D, [I, I, I, I, I, U64, P]),
             "or_set_accel_noise": (None, [D, U64]), "or_set_solver_tol": (None, [D]),
+            "or_set_probe": (None, [I, D, U64]),
             "or_ik_arm_init_flat": (None, [P, P]), "or_ik_arm_reset_flat": (None, [P, P]),
             "or_ik_plan_flat": (I, [I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
             "or_ik_finish_flat": (None, [P, P, I, P, I, P]),
@@ -106,7 +107,8 @@ def _bind(L, real):
             "or_compose_class": (None, [P, I, P, P, P, P, P, P]),
             "or_t_set_ignore": (None, [P, I, P, I]), "or_t_set_in_scene": (None, [P, P, I]),
             "or_t_set_scores": (None, [P, I, I]), "or_t_reset_reward_state": (None, [P]), "or_t_set_act_dim": (None, [P, I]),
-            "or_env_act_dim": (I, [P]), "or_env_ik_steps": (I, [P]), "or_env_ik_arm": (None, [P, I, P, P]),
+            "or_env_act_dim": (I, [P]), "or_env_ik_steps": (I, [P]),
+            "or_env_ik_calls": (C.c_long, [P, I]), "or_env_ik_fails": (C.c_long, [P, I]), "or_env_ik_arm": (None, [P, I, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -377,6 +379,10 @@ class Env:
 
     def ik_steps(self):
         return self.L.or_env_ik_steps(self.h)
+
+    def ik_solve_counts(self, arm):
+        """(IK solves, failed solves) of arm `arm` since creation (diagnostics)"""
+        return int(self.L.or_env_ik_calls(self.h, arm)), int(self.L.or_env_ik_fails(self.h, arm))
 
     def export_state(self):
         """full arena state in the product's record layout (fm_get_state)"""

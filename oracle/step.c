@@ -85,8 +85,31 @@ void or_fwd_acceleration(const or_model* m, or_data* d) {
   or_chol_solve_env(L, nv, f, d->qacc_smooth);
 }
 
+/* data-precision probe (tools/fp32_floor.py --probe, not part of the restated algorithm): a relative perturbation
+ * amp*U(-1,1) of chosen inputs of the substep's dynamics, modelling one fp32 rounding of each entry -- bit 1 the
+ * constraint Jacobian, 2 the mass matrix (symmetric), 4 qacc_smooth, 8 efc_D, 16 efc_aref, 32 qfrc_bias */
+static double g_probe_amp = 0.0;
+static int g_probe_mask = 0;
+static double noise_u(void);
+void or_set_probe(int mask, double amp, uint64_t seed);
+static void probe(double* x, int n, int bit) {
+  if (!(g_probe_mask & bit)) return;
+  for (int i = 0; i < n; i++) x[i] *= 1.0 + g_probe_amp * noise_u();
+}
+static void probe_sym(double* A, int n, int bit) {
+  if (!(g_probe_mask & bit)) return;
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j <= i; j++) {
+      A[i * n + j] *= 1.0 + g_probe_amp * noise_u();
+      A[j * n + i] = A[i * n + j];
+    }
+}
+
 static void fwd_constraint(const or_model* m, or_data* d) {
   int nv = m->nv;
+  probe(d->efc_J, d->nefc * nv, 1);
+  probe(d->efc_D, d->nefc, 8);
+  probe(d->efc_aref, d->nefc, 16);
   if (d->nefc == 0) {
     memcpy(d->qacc, d->qacc_smooth, nv * sizeof(double));
     memcpy(d->qacc_warmstart, d->qacc_smooth, nv * sizeof(double));
@@ -112,6 +135,11 @@ static double g_acc_noise = 0.0;
 static uint64_t g_noise_state = 0x9E3779B97F4A7C15ull;
 void or_set_accel_noise(double amp, uint64_t seed) {
   g_acc_noise = amp;
+  g_noise_state = seed * 0x9E3779B97F4A7C15ull + 1;
+}
+void or_set_probe(int mask, double amp, uint64_t seed) {
+  g_probe_mask = mask;
+  g_probe_amp = amp;
   g_noise_state = seed * 0x9E3779B97F4A7C15ull + 1;
 }
 static double noise_u(void) { /* xorshift64*, uniform in [-1, 1) */
@@ -160,7 +188,10 @@ void or_implicit(const or_model* m, or_data* d) {
 
 void or_step2(const or_model* m, or_data* d) {
   or_fwd_actuation(m, d);
+  probe(d->qfrc_bias, m->nv, 32);
+  probe_sym(d->M, m->nv, 2);
   or_fwd_acceleration(m, d);
+  probe(d->qacc_smooth, m->nv, 4);
   fwd_constraint(m, d);
   or_implicit(m, d);
 }

@@ -379,6 +379,8 @@ static int env_ik_solve(void* ctx, int arm, const double* tp, const double* tq, 
   int steps = 0;
   int ok = or_ik_solve(e->m, e->ik_d, e->d->qpos, arm, tp, tq, q7, &steps);
   e->ik_steps += steps;
+  e->ik_calls[arm]++;
+  if (!ok) e->ik_fails[arm]++;
   return ok;
 }
 

@@ -3,12 +3,11 @@
 * The four saved PPO runs (runs/*.zip -> tests/golden/policy_<run>.npz): each run's ep_info_buffer holds the
   Monitor (r, l) of its last 100 training episodes in MuJoCo (tests/golden/runs_fixtures.npz); the same policy
   (SB3 predict, stochastic) drives the GPU env from reset, one episode per arena.
-* The IK base policy (FactoryManipulationEnv, 2 arms): report/report.tex:276-295 quotes mean scores (1.65, 1.17)
-  and a mean length of 208.8 over 100 episodes (visualisation.py:55-85).
+* The IK base policy (FactoryManipulationEnv): report/report.tex:276-295 quotes mean scores (1.65, 1.17) and a mean
+  length of 208.8 over 100 sequential episodes for 2 arms (visualisation.py:55-85), (1.18, 1.16) / 119.74 for 4.
 
-The bands are the measured agreement (behaviour): a policy's return and length within a few percent of
-its training episodes; the IK base policy's length within 15 % and its summed score within 30 % of the report (the
-report's run is 100 sequential episodes of one seed; its arm asymmetry is not reproduced here)."""
+The bands: a policy's return and length within a few percent of its training episodes (measured agreement, DESIGN.md
+§3); the base policy per bucket and in length within 2.5 combined standard errors of the report."""
 import json
 import os
 import sys
@@ -49,17 +48,44 @@ def test_saved_policy_return_and_length_match_training_episodes(run):
     assert abs(out["l"]["mean"] / ref["l"]["mean"] - 1) <= bl, (out["l"], ref["l"])
 
 
+def _within(mean, se, ref, ref_se, k=2.5):
+    """|mean - ref| within k combined standard errors (ours and the report's 100-episode sample)"""
+    return abs(mean - ref) <= k * np.hypot(se, ref_se)
+
+
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-@pytest.mark.parametrize("A,length,scores", [(2, 208.8, (1.65, 1.17)), (4, 119.74, (1.18, 1.16))])
-def test_ik_base_policy_against_the_report(A, length, scores):
-    """report.tex:276-295 (measured here: 2 arms (1.72, 1.70) in 232.7 steps, 4 arms (1.05, 0.95) in 109.6)"""
+def test_ik_base_policy_report_protocol_two_arms():
+    """report.tex:276-282 under its own protocol (visualisation.py:55-80): one FactoryManipulationEnv, seed 42, 100
+    sequential episodes with the TaskManager RNG running on, length = t.  Each bucket's mean score and the mean length
+    within 2.5 combined standard errors of the report's (1.65, 1.17) / 208.8 -- the report's standard errors are not
+    quoted; ours (same protocol, same n) stand in for them.  The oracle under this protocol
+    (profiles/r04_base_policy_2arms_oracle.json, tools/base_policy_study.py): (1.56 +- 0.14, 1.35 +- 0.14), 213.1 +-
+    10.5, with the per-arm breakdown of the asymmetry (arm 1 plans after arm 0 and ignores its target: fewer grasp
+    attempts, most of the timeouts)"""
     import behaviour
 
-    out = behaviour.base(types.SimpleNamespace(A=A, arenas=512, episodes=0, precision="fp32"))
+    out = behaviour.base(types.SimpleNamespace(A=2, arenas=0, episodes=100, precision="fp32"))
+    seq = out["sequential"]
+    print(json.dumps(seq))
+    assert seq["episodes"] == 100
+    s0, s1, ln = seq["scores0"], seq["scores1"], seq["length_t"]
+    assert _within(s0["mean"], s0["se"], 1.65, s0["se"]), s0
+    assert _within(s1["mean"], s1["se"], 1.17, s1["se"]), s1
+    assert _within(ln["mean"], ln["se"], 208.8, ln["se"]), ln
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_ik_base_policy_four_arms_against_the_report():
+    """report.tex:289-295 base row (1.18, 1.16) / 119.74, 4 arms: the large-sample estimate (512 arenas of seeds
+    42 + i, first episode each; measured (1.05, 0.95) in 109.6) per bucket within 2.5 combined standard errors, the
+    report's taken as the oracle's under the report's protocol (profiles/r04_base_policy_4arms_oracle.json: 0.14,
+    0.12, 7.8)"""
+    import behaviour
+
+    out = behaviour.base(types.SimpleNamespace(A=4, arenas=512, episodes=0, precision="fp32"))
     par = out["parallel"]
     print(json.dumps(par))
     assert par["finished"] == 512
-    score = par["scores0"]["mean"] + par["scores1"]["mean"]
-    assert abs(par["length_t"]["mean"] / length - 1) <= 0.15, par["length_t"]
-    assert abs(score / sum(scores) - 1) <= 0.30, score
-    assert np.isfinite(score)
+    assert _within(par["scores0"]["mean"], par["scores0"]["se"], 1.18, 0.14), par["scores0"]
+    assert _within(par["scores1"]["mean"], par["scores1"]["se"], 1.16, 0.12), par["scores1"]
+    assert _within(par["length_t"]["mean"], par["length_t"]["se"], 119.74, 7.8), par["length_t"]

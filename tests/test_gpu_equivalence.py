@@ -165,3 +165,4 @@ def test_one_pass_warmstart_products_are_exact(precision):
     (FM_TWO_PASS_SETUP=1): the same products per row, so 40 env-steps of 256 arenas are bit-identical"""
     a, b = _run(2, 4, 256, 40, "FM_TWO_PASS_SETUP", precision=precision)
     assert np.array_equal(a, b)
+

@@ -105,7 +105,54 @@ def summarize(rows, gate=1e-4):
                 missing_steps=[r["step"] for r in rows if r["err"] is not None and r["err"] > gate])
 
 
+def cached_study(spec, mode="noise", amp=2.0 ** -24, seed=1):
+    """the probes on a cached teacher-forced trajectory of any env class (tools/parity_sweep.py load_traj, spec
+    A,K,T,seed[,EnvClass]): from each recorded state, mode "noise" = the float64 oracle with every substep's
+    acceleration scaled by 1 + amp U(-1, 1); mode "float" = the float restatement from the state rounded to float32;
+    compared with the recorded float64 step"""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    from parity_sweep import _parse, load_traj
+
+    from factory_marl_amd import state as st
+
+    A, K, T, sd, env_class, _ = _parse(spec)
+    recs, acts, outs = load_traj(A, K, T, sd, env_class)
+    p = po.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4), env_class=env_class, f32=(mode == "float"))
+    p.reset()
+    rows = []
+    for k in range(len(recs)):
+        d, i, r = st.unpack(A, K, recs[k])
+        if mode == "float":
+            p.import_state(d.astype(np.float32), i, r)
+        elif mode == "noise":
+            p.import_state(d, i, r)
+            po.lib().or_set_accel_noise(amp, seed + k)
+        else:  # "probe:MASK": one rounding of the chosen inputs of every substep (oracle/step.c or_set_probe)
+            p.import_state(d, i, r)
+            po.lib().or_set_probe(int(mode.split(":")[1]), amp, seed + k)
+        _, _, term, _, info = p.step(acts[k])
+        po.lib().or_set_accel_noise(0.0, 0)
+        po.lib().or_set_probe(0, 0.0, 0)
+        d2, i2, _ = p.export_state()
+        o = outs[k]
+        flip = (term != o["term"]) or not np.array_equal(i2, o["ints"])
+        rows.append(dict(step=k, err=None if o["term"] else rel_err(A, K, d2.astype(np.float64), o["dbl"]),
+                         term=bool(o["term"]), flip=bool(flip), ncubes=int(info["num_obj"])))
+    return rows
+
+
 if __name__ == "__main__":
+    if "--cached" in sys.argv:
+        # python tools/fp32_floor.py --cached SPEC [--float] : the probes on a cached trajectory (any env class)
+        spec = sys.argv[sys.argv.index("--cached") + 1]
+        mode = "float" if "--float" in sys.argv else "noise"
+        if "--probe" in sys.argv:  # bit mask: 1 J, 2 M, 4 qacc_smooth, 8 D, 16 aref, 32 qfrc_bias
+            mode = "probe:" + sys.argv[sys.argv.index("--probe") + 1]
+        po.build()
+        amp = float(sys.argv[sys.argv.index("--amp") + 1]) if "--amp" in sys.argv else 2.0 ** -24
+        print(json.dumps(dict(traj=spec, probe=mode, amp=amp, **summarize(cached_study(spec, mode, amp)))), flush=True)
+        sys.exit(0)
     argv = sys.argv[1:]
     noise = 0.0
     if "--accel-noise" in argv:
