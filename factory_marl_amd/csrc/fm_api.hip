@@ -65,6 +65,7 @@ struct fm_handle {
   double* arm_base_w = nullptr;
   void* body = nullptr;
   void* dof = nullptr;
+  double* dofd = nullptr;
   void* ctrlrange = nullptr;
   void* geom = nullptr;
   void* geomd = nullptr;
@@ -107,7 +108,7 @@ struct fm_handle {
   char* bak = nullptr;
   Lay lay_rerun{};
   char* spill_buf = nullptr;   // [N][spill_stride]
-  long long spill_stride = 0;  // Lay::gtotal of the spill layout in use (runtime fp64 (4,16); FM_SPILL24 builds)
+  long long spill_stride = 0;  // Lay::gtotal of the spill layout in use (compile-time scenes; runtime fp64 (4,16))
 };
 
 template <typename T>
@@ -175,6 +176,7 @@ static Model<T> make_model(const fm_handle* h) {
   M.arm_base_w = h->arm_base_w;
   M.body = (const T*)h->body;
   M.dof = (const T*)h->dof;
+  M.dofd = h->dofd;
   M.ctrlrange = (const T*)h->ctrlrange;
   M.ctrlrange_d = h->ctrlrange_d;
   M.geom = (const T*)h->geom;
@@ -313,6 +315,7 @@ static int create_typed(fm_handle* h) {
   }
   if ((r = upload<T>(h, &h->body, body))) return r;
   if ((r = upload<T>(h, &h->dof, dof))) return r;
+  if ((r = upload_raw<double>(h, &h->dofd, dof))) return r;
   if ((r = upload<T>(h, &h->ctrlrange, ctrl))) return r;
   if ((r = upload_raw<double>(h, &h->ctrlrange_d, ctrl))) return r;
   if ((r = upload<T>(h, &h->geom, geom))) return r;
@@ -443,7 +446,7 @@ static int create_typed(fm_handle* h) {
 #undef X
   }
   (void)idx;
-  if (h->fixed >= 0 && h->lay_step.spill) {  // FM_SPILL24 experiment builds: the fixed scene's global scratch
+  if (h->fixed >= 0 && h->lay_step.spill) {  // compile-time scenes: the Hessian + contact records in global scratch
     h->spill_stride = h->lay_step.gtotal;
     HIPCHK(hipMalloc((void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay_step.gtotal));
     h->allocs.push_back(h->spill_buf);

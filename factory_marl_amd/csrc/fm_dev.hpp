@@ -63,6 +63,7 @@ struct Dims {
   static constexpr bool midcache = false;  // cached midphase (FixedDims of the large scenes)
   static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
   static constexpr bool rerun = false;      // see FixedDims<A, K, true>
+  static constexpr bool f64arms = false;    // see FixedDims
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -101,6 +102,7 @@ struct Model {
   cptr<double> arm_base_w;  // [A][12] the same in float64, world frame (IK base policy, fm_ik.hpp)
   cptr<T> body;      // [10][32] local pos(3) local R(9) mass ipos(3) iR(9) I(3) invw_t invw_r pad(2)
   cptr<T> dof;       // [9][4]   range lo, hi, dof_invweight0, pad
+  const double* dofd;  // [9][4]  the same in float64 (joint-limit rows)
   cptr<T> ctrlrange; // [nu][2]
   cptr<double> ctrlrange_d;  // [nu][2] float64 (actuator_ctrlrange as the reference clips with it)
   // geoms (compact, collidable)
@@ -236,6 +238,7 @@ struct Lay {
   int prof;   // uint64 [FM_NPROF]  phase clocks of this arena (profiling only)
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int mcache, mpos;  // cached midphase: uint32 [mc_cap(nv)] hit list, T [ncb][3] body positions at the build
+  int bposd, bRd;    // fp32 scenes with DIM::f64arms: double [A][10][3], [A][10][9] arm body poses (narrowphase)
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -498,7 +501,7 @@ __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4
 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
-                                              bool midcache = false, bool nobc = false) {
+                                              bool midcache = false, bool nobc = false, bool f64arms = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -571,6 +574,10 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
     L.mcache = take(4 * mc_cap(nv));
     L.mpos = take(tsize * 3 * ncb);
   }
+  if (f64arms && tsize == 4) {
+    L.bposd = take(8 * 30 * A);
+    L.bRd = take(8 * 90 * A);
+  }
   L.total = off;
   if (spill) {  // the two largest arrays in the arena's global scratch block (L2 / HBM) instead of LDS
     L.spill = 1;
@@ -595,22 +602,28 @@ struct DimsSpill : Dims {
 
 // WIDE_: the benchmark scene's rerun kernel -- the (2,4) scene at the wide contact capacity, stepping the arenas whose
 // env-step the 64-contact kernel abandoned at a stage with more contacts (State::rerun), so no contact is dropped
-#ifndef FM_SPILL24
-#define FM_SPILL24 0  // experiment builds: the (2,4) kernel's Hessian + contact records in global scratch (occupancy A/B)
-#endif
-#ifndef FM_SPILL416
-#define FM_SPILL416 0  // experiment builds: the same for the fp32 (4,16) kernel (155.9 KB of LDS: one arena per CU)
+// Compile-time scenes keep the Newton Hessian and the contact records -- the two largest arrays -- in a per-arena
+// global scratch block (L2-resident; a wave's global accesses are ordered like its LDS accesses, so SYNC() covers
+// their hand-offs), everything else in LDS: the arena workspace shrinks enough for more arenas per CU (round 4, one
+// box: (2,4) fp32 167.9k -> 197.1k env-steps/s with two waves per SIMD, fp64 81.9k -> 105.6k; (4,16) config 5
+// 9.5k -> 17.4k with four arenas per CU instead of one).  FM_SPILL_FIXED=0 (experiment builds): all in LDS.
+#ifndef FM_SPILL_FIXED
+#define FM_SPILL_FIXED 1
 #endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
-  static constexpr bool spill = (FM_SPILL24 && A_ == 2 && K_ == 4 && !WIDE_) || (FM_SPILL416 && A_ == 4 && K_ == 16);
+  static constexpr bool spill = FM_SPILL_FIXED && !WIDE_;
   static constexpr int A = A_, K = K_, nq = 1 + 7 * K_ + 9 * A_, nv = 1 + 6 * K_ + 9 * A_, nu = 1 + 8 * A_;
   static constexpr bool midcache = true;
   static constexpr int ngc = 13 + K_ + 55 * A_, ncb = 5 + A_ + K_ + 10 * A_, ntree = 1 + K_ + A_;
   static constexpr int maxrow = 10 * A_;
   static constexpr int MAXC = (A_ == 2 && K_ == 4 && !WIDE_) ? MAXCON : MAXCON_WIDE;
   static constexpr bool rerun = WIDE_;
+  // the fp32 (4,16) scene (config 5: IK grasps) keeps float64 arm body poses for the narrowphase: a float forward
+  // kinematics puts ~1e-7 m on the gripper / arm geoms' positions, which a contact on a cube turns into force errors
+  // (tools/fp32_floor.py --probe 64: 1e-7 m of geom noise alone drops the (4,16) Pause toggle to 90 % within)
+  static constexpr bool f64arms = A_ == 4 && K_ == 16;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
@@ -619,7 +632,7 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE);
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -184,6 +184,22 @@ struct Ws {
       return (double*)(base + L->qd);
     }
   }
+  __device__ __forceinline__ double* bposd() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (double*)(base + c.bposd);
+    } else {
+      return (double*)(base + L->bposd);
+    }
+  }
+  __device__ __forceinline__ double* bRd() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (double*)(base + c.bRd);
+    } else {
+      return (double*)(base + L->bRd);
+    }
+  }
   __device__ __forceinline__ double* vd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -1080,6 +1096,18 @@ __device__ __forceinline__ void geom_pose_f64(const Model<T>& M, const Ws<T, DIM
     R[8] = ww * ww - x * x - y * y + z * z;
     const T* cb = w.cube() + 4 * k;
     h[0] = h[1] = h[2] = (double)cb[0] + (double)cb[3];
+  } else if constexpr (DIM::f64arms) {
+    // the arm body's float64 pose (arm_pose_f64) and the geom's float64 local frame
+    const int arm = (kb - 2 - dm.K) / 10, b = (kb - 2 - dm.K) % 10;
+    const double* bp = w.bposd() + 30 * arm + 3 * b;
+    const double* bR = w.bRd() + 90 * arm + 9 * b;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      p[r] = bp[r] + bR[3 * r] * gg[0] + bR[3 * r + 1] * gg[1] + bR[3 * r + 2] * gg[2];
+#pragma unroll
+      for (int c = 0; c < 3; c++)
+        R[3 * r + c] = bR[3 * r] * gg[3 + c] + bR[3 * r + 1] * gg[6 + c] + bR[3 * r + 2] * gg[9 + c];
+    }
   } else {
     const T* x = w.gx() + 4 * g;
     p[0] = x[0];
@@ -1090,6 +1118,71 @@ __device__ __forceinline__ void geom_pose_f64(const Model<T>& M, const Ws<T, DIM
     matmul3(w.bR() + 90 * arm + 9 * b, M.geom + 16 * g + 3, Rf);
 #pragma unroll
     for (int k = 0; k < 9; k++) R[k] = Rf[k];
+  }
+}
+
+// float64 poses of arm `arm`'s ten bodies (the fp32 build's DIM::f64arms scenes, for the narrowphase): the serial
+// chain of arm_chain (iiwa14.xml:55-147, gripper.xml:4-44) from the float64 master state, the float64 base frame and
+// the arm template's float64 constants, in the kernel frame (z - zshift)
+template <typename T, typename DIM>
+__device__ __forceinline__ void arm_pose_f64(const Model<T>& M, const Ws<T, DIM>& w, int arm) {
+  const DIM dm(M.dm);
+  const double* qa = w.qd() + 1 + 7 * dm.K + 9 * arm;
+  const double* base = M.arm_base_w + 12 * arm;
+  double* bpos = w.bposd() + 30 * arm;
+  double* bR = w.bRd() + 90 * arm;
+  double Pp[3] = {base[0], base[1], base[2] - zshift<T>()}, PR[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) PR[k] = base[3 + k];
+  double Gp[3], GR[9];
+#pragma unroll
+  for (int b = 0; b < 10; b++) {
+    const double* bl = ARM_BODY[b];
+    if (b >= 8) {  // both plates hang off the gripper base
+#pragma unroll
+      for (int k = 0; k < 3; k++) Pp[k] = Gp[k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) PR[k] = GR[k];
+    }
+    double o[3], Rpre[9], R[9];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      o[r] = Pp[r] + PR[3 * r] * bl[0] + PR[3 * r + 1] * bl[1] + PR[3 * r + 2] * bl[2];
+#pragma unroll
+      for (int c = 0; c < 3; c++)
+        Rpre[3 * r + c] = PR[3 * r] * bl[3 + c] + PR[3 * r + 1] * bl[6 + c] + PR[3 * r + 2] * bl[9 + c];
+    }
+    if (b < 7) {
+      double sn, cs;
+      sincos(qa[b], &sn, &cs);
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        R[3 * r + 0] = Rpre[3 * r + 0] * cs + Rpre[3 * r + 1] * sn;
+        R[3 * r + 1] = -Rpre[3 * r + 0] * sn + Rpre[3 * r + 1] * cs;
+        R[3 * r + 2] = Rpre[3 * r + 2];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = Rpre[k];
+      if (b >= 8) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) o[k] += Rpre[3 * k] * qa[b - 1];  // slide along the plate's local x
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) bpos[3 * b + k] = o[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) bR[9 * b + k] = R[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) Pp[k] = o[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) PR[k] = R[k];
+    if (b == 7) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) Gp[k] = o[k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) GR[k] = R[k];
+    }
   }
 }
 
@@ -2288,6 +2381,9 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     pb[3] = pb[4] = pb[5] = 0;
   }
   if (LANE == 0) w.pb()[0] = -M.belt_damp * v[0];  // belt: damping, no gravity along y
+  if constexpr (DIM::f64arms && sizeof(T) == 4) {
+    if (LANE < A) arm_pose_f64(M, w, LANE);
+  }
   SYNC();
   if (!fk_scan) {
     // per-body com / inertia / RNE forces one lane per (arm, body), then the RNE backward sum one lane per arm
@@ -2517,7 +2613,11 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
       const int cand = c00 + LANE;
       bool act = false, eq = false;
       int d0 = 0, d1 = -1;
-      T c0 = 0, c1 = 0, pos = 0, diag = 0;
+      T c0 = 0, c1 = 0, diag = 0;
+      // the constraint violation from the float64 master state and float64 limits: the plates' equality is a
+      // difference of two ~0.06 m slides (a float difference keeps ~7e-9 m of a ~1e-7 m violation)
+      double pos = 0.0;
+      const double* qd = w.qd();
       if (cand < PER * A) {
         const int arm = cand / PER, k = cand - PER * arm;
         const int qa = 1 + 7 * K + 9 * arm, va = 1 + 6 * K + 9 * arm;
@@ -2527,15 +2627,15 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
           d1 = va + 8;
           c0 = T(1);
           c1 = T(-1);
-          pos = q[qa + 7] - q[qa + 8];
+          pos = qd[qa + 7] - qd[qa + 8];
           diag = M.dof[4 * 7 + 2] + M.dof[4 * 8 + 2];
         } else {
           const int d = (k - 1) >> 1;
           const bool upper = (k - 1) & 1;
-          const T qv = q[qa + d];
-          pos = upper ? M.dof[4 * d + 1] - qv : qv - M.dof[4 * d];
+          const double qv = qd[qa + d];
+          pos = upper ? M.dofd[4 * d + 1] - qv : qv - M.dofd[4 * d];
           c0 = upper ? T(-1) : T(1);
-          act = pos < T(0);
+          act = pos < 0.0;
           d0 = va + d;
           diag = M.dof[4 * d + 2];
         }
@@ -2552,15 +2652,16 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
         ri[2] = eq ? 0 : 1;  // 0 equality, 1 inequality
         rr[RR_C0] = c0;
         rr[RR_C1] = c1;
-        rr[RR_POS] = pos;
-        const double imp = impedance(si, (double)pos);
+        rr[RR_POS] = (T)pos;
+        const double imp = impedance(si, pos);
         double Kk, Bb;
         kb_params(M.timestep, sr, si, Kk, Bb);
         double R = (1.0 - imp) * (double)diag / imp;
         R = R > 1e-15 ? R : 1e-15;
         rr[RR_D] = (T)(1.0 / R);
-        const double vel = (double)c0 * (double)v[d0] + (d1 >= 0 ? (double)c1 * (double)v[d1] : 0.0);
-        rr[RR_AREF] = (T)(-Bb * vel - Kk * imp * (double)pos);
+        const double* vd = w.vd();
+        const double vel = (double)c0 * vd[d0] + (d1 >= 0 ? (double)c1 * vd[d1] : 0.0);
+        rr[RR_AREF] = (T)(-Bb * vel - Kk * imp * pos);
       }
       nr += __popcll(bal);
     }
@@ -4453,23 +4554,26 @@ __device__ __forceinline__ void smooth_acc(const Model<T>& M, const Ws<T, DIM>& 
   int a0 = 1 + 6 * K;
   for (int i = LANE; i < a0; i += WAVE) w.as()[i] = w.fs()[i] / Mdiag(M, w, i);
   if (LANE < dm.A) {
+    // the arm block in float64 (both builds): with the gripper plates' small masses in it the block's Cholesky loses
+    // ~4 digits in float (qacc_smooth of the plate dofs off by 2e-4 relative, tools/miss_probe.py), and qacc_smooth
+    // sets the solver's optimum through the cost's M-norm term
     const T* Mb = w.Marm() + 81 * LANE;
-    T Lp[45], x[9];
+    double Lp[45], x[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) {
 #pragma unroll
-      for (int j = 0; j <= i; j++) Lp[P9(i, j)] = Mb[9 * i + j];
-      x[i] = w.fs()[a0 + 9 * LANE + i];
+      for (int j = 0; j <= i; j++) Lp[P9(i, j)] = (double)Mb[9 * i + j];
+      x[i] = (double)w.fs()[a0 + 9 * LANE + i];
     }
     spd9_solve(Lp, x);
 #pragma unroll
-    for (int k = 0; k < 9; k++) w.as()[a0 + 9 * LANE + k] = x[k];
+    for (int k = 0; k < 9; k++) w.as()[a0 + 9 * LANE + k] = (T)x[k];
   }
   SYNC();
 }
 
 #ifndef FM_INT_F64
-#define FM_INT_F64 0  // experiment: the implicitfast acceleration solve in float64 for the fp32 build
+#define FM_INT_F64 1  // the implicitfast acceleration solve in float64 in the fp32 build (the arm blocks' plates, as in smooth_acc)
 #endif
 template <typename T, typename DIM>
 __device__ __forceinline__ void implicit_integrate(const Model<T>& M, const Ws<T, DIM>& w, int arena, bool actuation) {
@@ -5043,10 +5147,9 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
 #else
 #define FM_STEP_ATTR
 #endif
+// one env-step of one arena on the calling wave (the body of step_kernel)
 template <typename T, typename DIM, bool IK>
-__global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> params) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  (void)params;
+__device__ __forceinline__ void step_arena(char* smem, const int arena) {
   // All launch parameters are read through an opaque pointer to the kernarg segment at each use, so the
   // compiler cannot hoist the ~50 scalar values out of the substep loop and run out of SGPRs.
   // The pointer stays in the constant address space (scalar loads, no FLAT instructions).
@@ -5054,20 +5157,6 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
 #define S (kparams<StepParams<T>>().S)
 #define io (kparams<StepParams<T>>().io)
 #define L (kparams<StepParams<T>>().L)
-  // longest-processing-time-first dispatch: the host orders the arenas by their last env-step's duration, so the
-  // expensive ones start in the first wave of workgroups and the cheap ones fill the tail (results do not depend
-  // on which workgroup steps an arena)
-  int arena_sel;
-  if constexpr (DIM::rerun) {
-    // the wide-capacity rerun: workgroup b steps the b-th arena the 64-contact launch abandoned (none: exit)
-    const int32_t* const rr = S.rerun;
-    if ((int)blockIdx.x >= rr[0]) return;
-    arena_sel = rr[1 + blockIdx.x];
-  } else {
-    const int32_t* const order_ = S.order;
-    arena_sel = order_ ? order_[blockIdx.x] : (int)blockIdx.x;
-  }
-  const int arena = arena_sel;
   const unsigned long long t_begin = wall_clock64();
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K, nu = dm.nu;
@@ -5337,6 +5426,28 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
 #undef act
 #undef phw
 #undef lp
+}
+
+template <typename T, typename DIM, bool IK>
+__global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> params) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  (void)params;
+  if constexpr (DIM::rerun) {
+    // the wide-capacity rerun: the arenas the 64-contact launch abandoned, S.rerun[1 + i] for i < S.rerun[0], over
+    // the launch's workgroups (a small grid: the list is short, usually empty)
+    const int32_t* const rr = kparams<StepParams<T>>().S.rerun;
+    const int n = rr[0];
+    for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
+      step_arena<T, DIM, IK>(smem, rr[1 + i]);
+      FULL_SYNC();
+    }
+  } else {
+    // longest-processing-time-first dispatch: the host orders the arenas by their last env-step's duration, so the
+    // expensive ones start in the first wave of workgroups and the cheap ones fill the tail (results do not depend
+    // on which workgroup steps an arena)
+    const int32_t* const order_ = kparams<StepParams<T>>().S.order;
+    step_arena<T, DIM, IK>(smem, order_ ? order_[blockIdx.x] : (int)blockIdx.x);
+  }
 }
 
 

@@ -20,10 +20,11 @@
 
 namespace fm {
 
-// the benchmark scene keeps 4 arenas (one wave per SIMD) per CU: its fp32 workspace must stay within a quarter of
-// the CU's 160 KiB of LDS (the midphase cache was sized to fit, fm_dev.hpp mc_cap)
-static_assert(!(FM_A == 2 && FM_K == 4 && FM_PREC == 32) || FixedDims<2, 4>::template layout<4>().total <= 160 * 1024 / 4,
-              "(2,4) fp32 workspace above 40 KiB: 3 arenas per CU");
+// the benchmark scene runs two waves (arenas) per SIMD, 8 per CU (FM_WAVES_PER_EU=2 for its objects, Makefile): its
+// workspace must stay within an eighth of the CU's 160 KiB of LDS with the Hessian and contact records spilled
+static_assert(!(FM_A == 2 && FM_K == 4 && FM_PREC == 32 && FM_SPILL_FIXED) ||
+                  FixedDims<2, 4>::template layout<4>().total <= 160 * 1024 / 8,
+              "(2,4) fp32 workspace above 20 KiB: fewer than 8 arenas per CU");
 
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes) {
@@ -44,8 +45,9 @@ void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStre
 }
 
 #if FM_WIDE
-// the benchmark scene's wide-capacity rerun (FixedDims<A, K, true>): workgroup b steps arena S.rerun[1 + b] when
-// b < S.rerun[0]; launched with one workgroup per arena of the handle, so every abandoned arena has its workgroup
+// the benchmark scene's wide-capacity rerun (FixedDims<A, K, true>): the workgroups step the arenas S.rerun[1 + i],
+// i < S.rerun[0], in a grid-stride loop; a small grid (the list is short and usually empty: one workgroup per arena
+// of the handle cost 2.5 % of the config-2 env-step in dispatch alone, gpurun_out/r04c quick_c vs quick_c_norerun)
 template <typename T, int A, int K>
 hipError_t rerun_set_attr() {
   const int lds = FixedDims<A, K, true>::template layout<sizeof(T)>().total;
@@ -64,10 +66,11 @@ Lay rerun_layout() {
 template <typename T, int A, int K>
 void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik) {
   const int lds = FixedDims<A, K, true>::template layout<sizeof(T)>().total;
+  const dim3 grid(num_arenas < 256 ? num_arenas : 256);
   if (ik)
-    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, true>), dim3(num_arenas), dim3(WAVE), lds, stream, p);
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, true>), grid, dim3(WAVE), lds, stream, p);
   else
-    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, false>), dim3(num_arenas), dim3(WAVE), lds, stream, p);
+    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, false>), grid, dim3(WAVE), lds, stream, p);
 }
 
 static_assert(FixedDims<FM_A, FM_K, true>::template layout<sizeof(FM_REAL)>().total <= 160 * 1024,

@@ -43,9 +43,39 @@ void or_velocity_stage(const or_model* m, or_data* d) {
   or_bias(m, d);
 }
 
+/* data-precision probe (tools/fp32_floor.py --probe, not part of the restated algorithm): a relative perturbation
+ * amp*U(-1,1) of chosen inputs of the substep's dynamics, modelling one fp32 rounding of each entry -- bit 1 the
+ * constraint Jacobian, 2 the mass matrix (symmetric), 4 qacc_smooth, 8 efc_D, 16 efc_aref, 32 qfrc_bias; 64 the
+ * arm / gripper geoms' world positions (absolute noise amp metres: float forward kinematics) before the collision,
+ * 128 their orientation matrices (absolute noise amp) */
+static double g_probe_amp = 0.0;
+static int g_probe_mask = 0;
+static double noise_u(void);
+void or_set_probe(int mask, double amp, uint64_t seed);
+static void probe(double* x, int n, int bit) {
+  if (!(g_probe_mask & bit)) return;
+  for (int i = 0; i < n; i++) x[i] *= 1.0 + g_probe_amp * noise_u();
+}
+static void probe_sym(double* A, int n, int bit) {
+  if (!(g_probe_mask & bit)) return;
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j <= i; j++) {
+      A[i * n + j] *= 1.0 + g_probe_amp * noise_u();
+      A[j * n + i] = A[i * n + j];
+    }
+}
+
 void or_step1(const or_model* m, or_data* d) {
   or_kinematics(m, d);
   or_mass(m, d);
+  if (g_probe_mask & (64 | 128))
+    for (int a = 0; a < m->A; a++)
+      for (int g = m->arm_geom_lo[a]; g < m->arm_geom_hi[a]; g++) {
+        if (g_probe_mask & 64)
+          for (int k = 0; k < 3; k++) d->geom_xpos[3 * g + k] += g_probe_amp * noise_u();
+        if (g_probe_mask & 128)
+          for (int k = 0; k < 9; k++) d->geom_xmat[9 * g + k] += g_probe_amp * noise_u();
+      }
   or_collision(m, d);
   or_make_constraint(m, d);
   transmission(m, d);
@@ -83,26 +113,6 @@ void or_fwd_acceleration(const or_model* m, or_data* d) {
   or_cholesky_env(L, nv, f);
   memcpy(d->qacc_smooth, d->qfrc_smooth, nv * sizeof(double));
   or_chol_solve_env(L, nv, f, d->qacc_smooth);
-}
-
-/* data-precision probe (tools/fp32_floor.py --probe, not part of the restated algorithm): a relative perturbation
- * amp*U(-1,1) of chosen inputs of the substep's dynamics, modelling one fp32 rounding of each entry -- bit 1 the
- * constraint Jacobian, 2 the mass matrix (symmetric), 4 qacc_smooth, 8 efc_D, 16 efc_aref, 32 qfrc_bias */
-static double g_probe_amp = 0.0;
-static int g_probe_mask = 0;
-static double noise_u(void);
-void or_set_probe(int mask, double amp, uint64_t seed);
-static void probe(double* x, int n, int bit) {
-  if (!(g_probe_mask & bit)) return;
-  for (int i = 0; i < n; i++) x[i] *= 1.0 + g_probe_amp * noise_u();
-}
-static void probe_sym(double* A, int n, int bit) {
-  if (!(g_probe_mask & bit)) return;
-  for (int i = 0; i < n; i++)
-    for (int j = 0; j <= i; j++) {
-      A[i * n + j] *= 1.0 + g_probe_amp * noise_u();
-      A[j * n + i] = A[i * n + j];
-    }
 }
 
 static void fwd_constraint(const or_model* m, or_data* d) {
