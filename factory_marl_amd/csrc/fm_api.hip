@@ -142,6 +142,7 @@ static Model<T> make_model(const fm_handle* h) {
   M.dt = T(0.001);
   M.timestep = 0.001;
   M.grav = T(9.81);
+  M.grav_d = 9.81;
   M.belt_mass = T(1000);
   M.belt_kv = T(1e4);
   M.belt_damp = T(5e-4);

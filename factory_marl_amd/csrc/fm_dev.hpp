@@ -89,6 +89,7 @@ struct Model {
   Dims dm;
   // scene scalars
   T dt, grav;
+  double grav_d;  // 9.81 exactly (a free cube's acceleration is -g: formed in float64, scene.xml default gravity)
   T belt_mass, belt_kv, belt_damp, belt_invw_t;
   double timestep;  // model.opt.timestep, exact (solver gains)
   double init_speed, accel, pt_time, force_thr, spawn_freq0, spawn_inc;

@@ -60,6 +60,36 @@ def run_episodes(env, act_fn, want_per_arena, max_steps):
     return eps, int(step + 1), int((done_count >= want_per_arena).sum())
 
 
+def sequential_episodes(env, episodes, chunk=2000, max_steps=200_000):
+    """the report's protocol on arena 0 (visualisation.py:55-80: env.reset() after each termination -- here the
+    kernel's auto-reset, which is reset_sim with the TaskManager RNG running on): per-step flags, terminal scores and
+    episode lengths are gathered on the device and read once per chunk (no host sync per env-step); returns the first
+    `episodes` episodes as (scores, length, return)"""
+    import torch
+
+    dev = env.device
+    a = torch.zeros(env.num_envs, env.act_dim, device=dev)  # FactoryManipulationEnv: no action entries
+    eps = []
+    done = 0
+    while len(eps) < episodes and done < max_steps:
+        term_h = torch.zeros(chunk, dtype=torch.bool, device=dev)
+        sc_h = torch.zeros(chunk, 2, dtype=torch.int32, device=dev)
+        len_h = torch.zeros(chunk, dtype=torch.int32, device=dev)
+        ret_h = torch.zeros(chunk, dtype=torch.float32, device=dev)
+        for t in range(chunk):
+            _, _, term, _ = env.step_tensors(a)
+            term_h[t] = term[0].bool()
+            sc_h[t] = env.terminal_scores[0]
+            len_h[t] = env.ep_len[0]
+            ret_h[t] = env.ep_return[0]
+        done += chunk
+        idx = torch.nonzero(term_h).flatten().cpu().numpy()
+        sc, ln, rt = sc_h.cpu().numpy(), len_h.cpu().numpy(), ret_h.cpu().numpy()
+        eps += [(sc[i].tolist(), int(ln[i]), float(rt[i])) for i in idx]
+        print(f"{done} env-steps: {len(eps)} episodes", file=sys.stderr, flush=True)
+    return eps[:episodes], done
+
+
 def base(args):
     import torch
 
@@ -75,7 +105,7 @@ def base(args):
                             return_numpy=False)
         env.reset()
         t0 = time.time()
-        eps, steps, _ = run_episodes(env, zero, args.episodes, args.episodes * 600)
+        eps, steps = sequential_episodes(env, args.episodes)
         env.close()
         out["sequential"] = dict(scores0=_stats([e[0][0] for e in eps]), scores1=_stats([e[0][1] for e in eps]),
                                  length_t=_stats([e[1] - 1 for e in eps]), episodes=len(eps),
