@@ -64,6 +64,7 @@ struct Dims {
   static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
   static constexpr bool rerun = false;      // see FixedDims<A, K, true>
   static constexpr bool f64arms = false;    // see FixedDims
+  static constexpr bool gl_lists = false;   // see FixedDims
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -502,7 +503,8 @@ __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4
 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
-                                              bool midcache = false, bool nobc = false, bool f64arms = false) {
+                                              bool midcache = false, bool nobc = false, bool f64arms = false,
+                                              bool gl_lists = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -554,7 +556,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   off = u0;
   L.gx = take(tsize * 4 * ngc);
   L.cbw = take(tsize * 8 * ncb);
-  L.sp = take(4 * (ncb * (ncb - 1) / 2));  // every possible body pair can pass the midphase
+  if (!gl_lists) L.sp = take(4 * (ncb * (ncb - 1) / 2));  // every possible body pair can pass the midphase
   L.gsurv = take(4 * 4 * WAVE);
   L.stage = take(tsize * 8 * maxcon);
   L.skey = take(4 * maxcon);
@@ -575,7 +577,8 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
     L.mcache = take(4 * mc_cap(nv));
     L.mpos = take(tsize * 3 * ncb);
   }
-  if (f64arms && tsize == 4) {
+  const bool f64a = f64arms && tsize == 4;
+  if (f64a && !gl_lists) {
     L.bposd = take(8 * 30 * A);
     L.bRd = take(8 * 90 * A);
   }
@@ -584,7 +587,18 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
     L.spill = 1;
     L.H = 0;
     L.c_r = (tsize * (hstride(tsize, nv) * hstride(tsize, nv) + hextra(tsize, nv)) + 15) & ~15;
-    L.gtotal = L.c_r + ((tsize * CR_N * maxcon + 255) & ~255);
+    int g = L.c_r + ((tsize * CR_N * maxcon + 255) & ~255);
+    if (gl_lists) {  // also the midphase hit list and the float64 arm poses (the (4,16) scene: 4 arenas per CU)
+      L.sp = g;
+      g += (4 * (ncb * (ncb - 1) / 2) + 255) & ~255;
+      if (f64a) {
+        L.bposd = g;
+        g += 8 * 30 * A;
+        L.bRd = g;
+        g += (8 * 90 * A + 255) & ~255;
+      }
+    }
+    L.gtotal = g;
   }
   return L;
 }
@@ -611,6 +625,9 @@ struct DimsSpill : Dims {
 #ifndef FM_SPILL_FIXED
 #define FM_SPILL_FIXED 1
 #endif
+#ifndef FM_GL_LISTS
+#define FM_GL_LISTS 1
+#endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
@@ -625,6 +642,9 @@ struct FixedDims {
   // kinematics puts ~1e-7 m on the gripper / arm geoms' positions, which a contact on a cube turns into force errors
   // (tools/fp32_floor.py --probe 64: 1e-7 m of geom noise alone drops the (4,16) Pause toggle to 90 % within)
   static constexpr bool f64arms = A_ == 4 && K_ == 16;
+  // the (4,16) scene also keeps its midphase hit list and float64 arm poses in the global block: 50.0 -> 37.9 KB of
+  // LDS, four arenas per CU instead of three
+  static constexpr bool gl_lists = spill && A_ == 4 && K_ == 16 && FM_GL_LISTS;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
@@ -633,7 +653,8 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms);
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms,
+                       gl_lists);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

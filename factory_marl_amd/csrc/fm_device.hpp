@@ -187,7 +187,7 @@ struct Ws {
   __device__ __forceinline__ double* bposd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (double*)(base + c.bposd);
+      return (double*)((DIM::gl_lists ? gbase : base) + c.bposd);
     } else {
       return (double*)(base + L->bposd);
     }
@@ -195,7 +195,7 @@ struct Ws {
   __device__ __forceinline__ double* bRd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (double*)(base + c.bRd);
+      return (double*)((DIM::gl_lists ? gbase : base) + c.bRd);
     } else {
       return (double*)(base + L->bRd);
     }
@@ -363,7 +363,7 @@ struct Ws {
   __device__ __forceinline__ uint32_t* sp() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (uint32_t*)(base + c.sp);
+      return (uint32_t*)((DIM::gl_lists ? gbase : base) + c.sp);
     } else {
       return (uint32_t*)(base + L->sp);
     }

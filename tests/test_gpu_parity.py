@@ -297,10 +297,11 @@ def test_masked_reset_only_touches_masked_arenas():
 
 
 # (4,16) fp32 gates per env class and oracle: (fraction within 1e-4, cap on the second-worst step, cap on the worst)
-# -- round 4 (profiles/r04_parity.md): against the 1e-8-tolerance oracle 99.32 % / 100 % within, worst 4.5e-4 / 3.5e-5;
-# against the 1e-12 oracle 98.65 % / 99.32 %, the Pause toggle's worst 0.92 at step 142, where the 1e-8 oracle takes
-# the kernel's branch (MuJoCo's tolerance, not precision)
-CONFIG5_GATES = {"PauseIKToggleEnv": {"1e-12": (0.98, 1e-3, 1.0), "1e-8": (0.99, 1e-3, 1e-3)},
+# -- round 4 (profiles/r04_parity.md): Backup 99.3 % / 100 % within against the 1e-12 / 1e-8 oracles, worst 5.5e-4 /
+# 3.9e-5; Pause 98.6 % against both, misses step 23 (4.5e-4) and step 142 -- a bifurcation where the 1e-12 and the
+# 1e-8 oracle themselves differ by 0.92 relative, and the kernel's branch follows one or the other with the last bits
+# of its arithmetic (it followed the 1e-8 oracle at r04d, the 1e-12 one at r04f)
+CONFIG5_GATES = {"PauseIKToggleEnv": {"1e-12": (0.98, 1e-3, 1.0), "1e-8": (0.98, 1e-3, 1.0)},
                  "BackupIKToggleEnv": {"1e-12": (0.99, 1e-3, 1e-3), "1e-8": (0.99, 1e-3, 1e-3)}}
 
 
