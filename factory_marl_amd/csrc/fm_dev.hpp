@@ -65,6 +65,7 @@ struct Dims {
   static constexpr bool rerun = false;      // see FixedDims<A, K, true>
   static constexpr bool f64arms = false;    // see FixedDims
   static constexpr bool gl_lists = false;   // see FixedDims
+  static constexpr bool treeblk = false;    // see FixedDims
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -241,6 +242,7 @@ struct Lay {
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int mcache, mpos;  // cached midphase: uint32 [mc_cap(nv)] hit list, T [ncb][3] body positions at the build
   int bposd, bRd;    // fp32 scenes with DIM::f64arms: double [A][10][3], [A][10][9] arm body poses (narrowphase)
+  int tblk;          // fp32 (4,16): the tree-block Newton solve's workspace (TB_* below; Newton-phase only)
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -501,10 +503,18 @@ __host__ __device__ constexpr int hstride(int tsize, int nv) { return (tsize == 
 // scratch floats after the padded Hessian (the dense Cholesky's inverse diagonal block)
 __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4 && nv > 80) ? 256 : 0; }
 
+// workspace of the tree-block Newton solve (fp32 (4,16)): per tree a 9 x 9 lower-triangle block (packed, P9) and its
+// belt row, then the coupled trees' dense system (<= TB_MAXR positions incl. the belt, row stride = its size) and its
+// position -> (tree, local dof) map
+constexpr int TB_BLK = 54, TB_MAXR = 32;
+__host__ __device__ constexpr int tb_rest(int ntree) { return (TB_BLK * ntree + 3) & ~3; }
+__host__ __device__ constexpr int tb_map(int ntree) { return tb_rest(ntree) + TB_MAXR * TB_MAXR; }
+__host__ __device__ constexpr int tb_floats(int ntree) { return tb_map(ntree) + TB_MAXR; }
+
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
                                               bool midcache = false, bool nobc = false, bool f64arms = false,
-                                              bool gl_lists = false) {
+                                              bool gl_lists = false, bool treeblk = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -552,6 +562,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.g = take(8 * nv);
   L.Ma = take(8 * nv);
   L.tmp = take(8 * nv);
+  if (treeblk) L.tblk = take(4 * tb_floats(ntree));
   int uend = off;
   off = u0;
   L.gx = take(tsize * 4 * ngc);
@@ -628,6 +639,9 @@ struct DimsSpill : Dims {
 #ifndef FM_GL_LISTS
 #define FM_GL_LISTS 1
 #endif
+#ifndef FM_TREEBLK
+#define FM_TREEBLK 1
+#endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
@@ -645,6 +659,9 @@ struct FixedDims {
   // the (4,16) scene also keeps its midphase hit list and float64 arm poses in the global block: 50.0 -> 37.9 KB of
   // LDS, four arenas per CU instead of three
   static constexpr bool gl_lists = spill && A_ == 4 && K_ == 16 && FM_GL_LISTS;
+  // the fp32 (4,16) scene solves the Newton system tree block by tree block (newton_treeblk): its dense 133-dof
+  // Hessian in the global block is only the fallback for more than TB_MAXR coupled positions
+  static constexpr bool treeblk = A_ == 4 && K_ == 16 && FM_TREEBLK;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
@@ -654,7 +671,7 @@ struct FixedDims {
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
     return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms,
-                       gl_lists);
+                       gl_lists, treeblk && TS == 4);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -160,6 +160,14 @@ struct Ws {
       return (double*)(base + L->tmp);
     }
   }
+  __device__ __forceinline__ float* tblk() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      return (float*)(base + c.tblk);
+    } else {
+      return (float*)(base + L->tblk);
+    }
+  }
   __device__ __forceinline__ T* fa() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -4089,6 +4097,316 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
   for (int i = LANE; i < dm.nv; i += WAVE) out[i] = (O)acc[i];
 }
 
+// ------------------------------------------------------------------------------------------------
+// Tree-block Newton solve of the fp32 (4,16) scene (config 5): H dir = -g without the dense 133-dof Hessian.
+// H couples two trees only through a contact between them (mass matrix: belt scalar, cubes diagonal, arm 9 x 9
+// blocks; generic rows stay inside one arm).  Elimination order: the single trees (no contact with another moving
+// tree except the belt), then the coupled trees, the belt last.  In that order H is block diagonal over the singles
+// with the coupled trees' block and a belt border, so
+//  * every single tree's 9 x 9 block (cubes padded with an identity) is factored on its own lane, serially in
+//    registers, together with its belt row l_t = L_t^-1 h_bt and its forward solve y_t = L_t^-1 (-g_t);
+//  * the rest -- the coupled trees (an arm grasping a cube, two cubes touching: 15-24 dofs measured on the oracle's
+//    PauseIKToggle trajectories) plus the belt, with the singles' Schur terms sum l_t'l_t and sum l_t'y_t folded into
+//    the belt's diagonal and right-hand side -- is one small dense system for the register Cholesky
+//    (chol_solve_reg<float, TB_MAXR>);
+//  * the singles' backward solves take the belt's solution from it.
+// The blocks are assembled in LDS (the Newton phase's share of the collision scratch): one lane per contact adds
+// B_a'K B_a, B_b'K B_b and the cross term B_a'K B_b (a belt row, the coupled system, or -- a contact inside one
+// tree -- the tree's own block) by LDS atomics; one lane per generic row likewise.  The same terms as the dense
+// assembly, summed in another order (fp32 rounding differs from the dense path; both are held to the oracle).
+// Returns false (nothing written but K_c) when more than TB_MAXR positions are coupled or a generic row couples two
+// trees: the caller runs the dense blocked factor.  Replaces the dense assembly + chol_dense_mfma, whose Hessian
+// lives in the arena's global block (round-4 phase profile: 44 + 117 us of 273 us per arena-substep).
+// gather_JtF by per-contact scatter (the compile-time scenes whose contact records live in the arena's global block:
+// (2,8), (2,10), (4,16)): one lane per contact adds its <= 18 column products J_c' f_c into the float64 accumulator by
+// LDS atomics, one lane per generic row likewise -- one round of record loads for up to 64 contacts, where the per-dof
+// walk over a tree's contacts is a chain of global-latency loads (the belt's lane walks every belt contact)
+template <typename T, typename DIM, typename O>
+__device__ __forceinline__ void gather_JtF_pc(const Model<T>& M, const Ws<T, DIM>& w, int ncon, int nrow, O* out,
+                                              double* acc) {
+  const DIM dm(M.dm);
+  for (int i = LANE; i < dm.nv; i += WAVE) acc[i] = 0.0;
+  SYNC();
+  for (int c = LANE; c < ncon; c += WAVE) {
+    const int* ci = w.ci() + 4 * c;
+    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+    const T* cr = w.cr() + CR_N * c;
+    const T* J = cr + CR_J;
+    const double* f3 = dslot(cr, CR_F3);
+    const double f0 = f3[0], f1 = f3[1], f2 = f3[2];
+    const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = (tb >= 0 ? tree_dof(dm, tb) : 0) - nda;
+    double v[CJ];
+#pragma unroll
+    for (int ii = 0; ii < CJ; ii++) v[ii] = (double)J[ii] * f0 + (double)J[CJ + ii] * f1 + (double)J[2 * CJ + ii] * f2;
+#pragma unroll
+    for (int ii = 0; ii < CJ; ii++)
+      if (ii < nda + ndb) atomicAdd(acc + (ii < nda ? oa : ob) + ii, v[ii]);
+  }
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    const T* rr = w.rr() + RR_N * r;
+    const double jar = *dslot(rr, RR_JAR);
+    if (!(ri[2] == 0 || jar < 0.0)) continue;
+    const double fr = (double)rr[RR_D] * jar;
+    atomicAdd(acc + ri[0], (double)rr[RR_C0] * fr);
+    if (ri[1] >= 0) atomicAdd(acc + ri[1], (double)rr[RR_C1] * fr);
+  }
+  SYNC();
+  for (int i = LANE; i < dm.nv; i += WAVE) out[i] = (O)acc[i];
+}
+template <typename T, typename DIM>
+__device__ constexpr bool pc_scene() {
+  if constexpr (DIM::fixed)
+    return DIM::spill && !(DIM::MAXC == WAVE && DIM::nv <= 48);  // not the (2,4) scene (its own scatter)
+  else
+    return false;
+}
+
+template <typename T, typename DIM>
+__device__ constexpr bool treeblk_scene() {
+  if constexpr (DIM::fixed && sizeof(T) == 4)
+    return DIM::treeblk;
+  else
+    return false;
+}
+__device__ __forceinline__ unsigned wave_or_u32(unsigned x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x |= (unsigned)__shfl_xor((int)x, o);
+  return x;
+}
+template <typename DIM>
+__device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<float, DIM>& w, const double* g,
+                                               float* dir, int ncon, int nrow) {
+  constexpr int NT = DIM::ntree, KK = DIM::K;
+  static_assert(NT <= 32 && DIM::nv <= 1 + 9 * (NT - 1), "one 32-bit tree mask; trees of <= 9 dofs");
+  const DIM dm(M.dm);
+  contact_K(w, ncon);
+  SYNC();
+  // ---- coupled trees: both moving trees (not the belt, not the world) of a contact with an active edge
+  unsigned cm = 0;
+  bool rowx = false;
+  for (int c = LANE; c < ncon; c += WAVE) {
+    const int* ci = w.ci() + 4 * c;
+    const int ta = ci[1], tb = ci[2];
+    if (ta > 0 && tb > 0 && ta != tb && w.cr()[CR_N * c + CR_K] != 0.0f) cm |= (1u << ta) | (1u << tb);
+  }
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    if (ri[1] >= 0 && dof_tree(dm, ri[0]) != dof_tree(dm, ri[1])) rowx = true;
+  }
+  cm = wave_or_u32(cm);
+  constexpr unsigned CUBES = ((1u << KK) - 1u) << 1;
+  const int m = 6 * __popc(cm & CUBES) + 9 * __popc(cm & ~CUBES);  // coupled positions (the belt excluded)
+  if (m + 1 > TB_MAXR || __ballot(rowx) != 0ull) return false;
+  const int n = m + 1;
+  // position of tree t's first dof in the coupled system (trees in index order: cubes, then arms)
+  auto cbase = [&](int t) {
+    const unsigned below = cm & ((1u << t) - 1u);
+    return 6 * __popc(below & CUBES) + 9 * __popc(below & ~CUBES);
+  };
+  float* const tbw = w.tblk();
+  float* const R = tbw + tb_rest(NT);
+  int* const cmap = (int*)(tbw + tb_map(NT));
+  // ---- zero the blocks, belt rows and the coupled system; the coupled system's position map
+  for (int e = LANE; e < TB_BLK * NT; e += WAVE) tbw[e] = 0.0f;
+  for (int e = LANE; e < n * n; e += WAVE) R[e] = 0.0f;
+  if (LANE > 0 && LANE < NT && ((cm >> LANE) & 1u)) {
+    const int b = cbase(LANE), nd = LANE <= KK ? 6 : 9;
+    for (int k = 0; k < nd; k++) cmap[b + k] = (LANE << 4) | k;
+  }
+  SYNC();
+  // ---- mass matrix: belt and cube diagonals, arm blocks (lower triangles)
+  for (int d = LANE; d < dm.nv; d += WAVE) {
+    const int t = dof_tree(dm, d), i = d - tree_dof(dm, t);
+    float* B = tbw + TB_BLK * t;
+    if (t <= KK) {
+      B[P9(i, i)] = Mdiag(M, w, d);
+    } else {
+      const float* Mr = w.Marm() + 81 * (t - 1 - KK) + 9 * i;
+      for (int j = 0; j <= i; j++) B[P9(i, j)] = Mr[j];
+    }
+  }
+  SYNC();
+  // ---- contacts: one lane per contact
+  for (int c = LANE; c < ncon; c += WAVE) {
+    const int* ci = w.ci() + 4 * c;
+    const float* cr = w.cr() + CR_N * c;
+    const float* Kc = cr + CR_K;
+    const float k0 = Kc[0], k1 = Kc[1], k2 = Kc[2], k3 = Kc[3], k4 = Kc[4], k5 = Kc[5];
+    if (k0 == 0.0f) continue;  // no active pyramid edge: no Hessian term
+    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+    const float* J = cr + CR_J;
+    float ja[3][9], jb[3][9], qa[3][9], qb[3][9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        ja[r][i] = J[r * CJ + i];
+        jb[r][i] = J[r * CJ + nda + i];  // nda + i <= 17 < CJ: inside the record
+      }
+      qa[0][i] = k0 * ja[0][i] + k3 * ja[1][i] + k4 * ja[2][i];
+      qa[1][i] = k3 * ja[0][i] + k1 * ja[1][i] + k5 * ja[2][i];
+      qa[2][i] = k4 * ja[0][i] + k5 * ja[1][i] + k2 * ja[2][i];
+      qb[0][i] = k0 * jb[0][i] + k3 * jb[1][i] + k4 * jb[2][i];
+      qb[1][i] = k3 * jb[0][i] + k1 * jb[1][i] + k5 * jb[2][i];
+      qb[2][i] = k4 * jb[0][i] + k5 * jb[1][i] + k2 * jb[2][i];
+    }
+    // own blocks of the two trees (a tree < 0 is the world: no columns)
+    if (ta >= 0) {
+      float* B = tbw + TB_BLK * ta;
+#pragma unroll
+      for (int i = 0; i < 9; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++)
+          if (i < nda) atomicAdd(B + P9(i, j), qa[0][i] * ja[0][j] + qa[1][i] * ja[1][j] + qa[2][i] * ja[2][j]);
+    }
+    if (tb >= 0) {
+      float* B = tbw + TB_BLK * tb;
+#pragma unroll
+      for (int i = 0; i < 9; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++)
+          if (i < ndb) atomicAdd(B + P9(i, j), qb[0][i] * jb[0][j] + qb[1][i] * jb[1][j] + qb[2][i] * jb[2][j]);
+    }
+    if (ta < 0 || tb < 0) continue;
+    // cross term B_a' K B_b: a belt row, a contact inside one tree, or an entry pair of the coupled system
+    if (tb == 0 || ta == 0) {
+      const bool bb = tb == 0;  // the belt is tree b: tree a's belt row, else tree b's
+      float* Bl = tbw + TB_BLK * (bb ? ta : tb) + 45;
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        const float v = bb ? qa[0][i] * jb[0][0] + qa[1][i] * jb[1][0] + qa[2][i] * jb[2][0]
+                           : qb[0][i] * ja[0][0] + qb[1][i] * ja[1][0] + qb[2][i] * ja[2][0];
+        if (i < (bb ? nda : ndb)) atomicAdd(Bl + i, v);
+      }
+    } else if (ta == tb) {
+      float* B = tbw + TB_BLK * ta;
+#pragma unroll
+      for (int i = 0; i < 9; i++)
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+          const float v = qa[0][i] * jb[0][k] + qa[1][i] * jb[1][k] + qa[2][i] * jb[2][k];
+          if (i < nda && k < ndb) atomicAdd(B + (i >= k ? P9(i, k) : P9(k, i)), i == k ? 2.0f * v : v);
+        }
+    } else {
+      const int ca = cbase(ta), cb = cbase(tb);
+#pragma unroll
+      for (int i = 0; i < 9; i++)
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+          const float v = qa[0][i] * jb[0][k] + qa[1][i] * jb[1][k] + qa[2][i] * jb[2][k];
+          if (i < nda && k < ndb) {
+            atomicAdd(R + (ca + i) * n + cb + k, v);
+            atomicAdd(R + (cb + k) * n + ca + i, v);
+          }
+        }
+    }
+  }
+  // ---- generic rows (gripper equality, joint limits: inside one tree), one lane per row
+  for (int r = LANE; r < nrow; r += WAVE) {
+    const int* ri = w.ri() + 4 * r;
+    const float* rr = w.rr() + RR_N * r;
+    if (!(ri[2] == 0 || *dslot(rr, RR_JAR) < 0.0)) continue;
+    const float D = rr[RR_D], c0 = rr[RR_C0], c1 = rr[RR_C1];
+    const int d0 = ri[0], d1 = ri[1], t = dof_tree(dm, d0), o = tree_dof(dm, t);
+    float* B = tbw + TB_BLK * t;
+    const int l0 = d0 - o;
+    atomicAdd(B + P9(l0, l0), D * c0 * c0);
+    if (d1 >= 0) {
+      const int l1 = d1 - o;
+      atomicAdd(B + P9(l1, l1), D * c1 * c1);
+      atomicAdd(B + (l0 >= l1 ? P9(l0, l1) : P9(l1, l0)), (l0 == l1 ? 2.0f : 1.0f) * D * c0 * c1);
+    }
+  }
+  SYNC();
+  PMARK(PH_NHESS);
+  // ---- single trees: lane t factors its block, its belt row and its forward solve in registers
+  const float tiny = 1e-37f;
+  const int t = LANE;
+  const bool single = t > 0 && t < NT && !((cm >> t) & 1u);
+  const bool cube = t <= KK;
+  const int d0 = t < NT ? tree_dof(dm, t) : 0;
+  float Lb[45], dv[9], lb[9], y[9];
+  float s_t = 0.0f, ly_t = 0.0f;
+  if (single) {
+    const float* B = tbw + TB_BLK * t;
+#pragma unroll
+    for (int k = 0; k < 45; k++) Lb[k] = B[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) lb[k] = B[45 + k];
+    if (cube) {  // identity padding of the cube's 6 x 6 block (its rows 6..8 and belt entries 6..8 are zero)
+      Lb[P9(6, 6)] = 1.0f;
+      Lb[P9(7, 7)] = 1.0f;
+      Lb[P9(8, 8)] = 1.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      float d = Lb[P9(k, k)];
+      d = d > tiny ? d : tiny;
+      const float ri = 1.0f / sqrtf(d);
+      dv[k] = ri;
+#pragma unroll
+      for (int i = k + 1; i < 9; i++) Lb[P9(i, k)] *= ri;
+#pragma unroll
+      for (int i = k + 1; i < 9; i++)
+#pragma unroll
+        for (int j = k + 1; j <= i; j++) Lb[P9(i, j)] -= Lb[P9(i, k)] * Lb[P9(j, k)];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      float a = lb[i], b = (cube && i >= 6) ? 0.0f : (float)-g[d0 + (i < 9 ? i : 0)];
+#pragma unroll
+      for (int k = 0; k < i; k++) {
+        a -= Lb[P9(i, k)] * lb[k];
+        b -= Lb[P9(i, k)] * y[k];
+      }
+      lb[i] = a * dv[i];
+      y[i] = b * dv[i];
+      s_t += lb[i] * lb[i];
+      ly_t += lb[i] * y[i];
+    }
+  }
+  const float S = wave_sum(s_t), LY = wave_sum(ly_t);
+  // ---- the coupled system + belt (position m), in LDS with row stride n
+  double* const grest = w.tmp();                  // right-hand side (chol_solve_reg negates it)
+  float* const xr = (float*)(w.tmp() + TB_MAXR);  // its solution
+  for (int e = LANE; e < n * n; e += WAVE) {
+    const int i = e / n, j = e - n * (e / n);
+    if (i < m && j < m) {
+      const int ti = cmap[i] >> 4, li = cmap[i] & 15, tj = cmap[j] >> 4, lj = cmap[j] & 15;
+      if (ti == tj) R[e] = tbw[TB_BLK * ti + (li >= lj ? P9(li, lj) : P9(lj, li))];
+    } else if (i == m && j == m) {
+      R[e] = tbw[0] - S;  // the belt's diagonal (block of tree 0) minus the singles' Schur terms
+    } else {
+      const int p = i == m ? j : i;
+      R[e] = tbw[TB_BLK * (cmap[p] >> 4) + 45 + (cmap[p] & 15)];
+    }
+  }
+  for (int i = LANE; i < n; i += WAVE)
+    grest[i] = i < m ? g[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] : g[0] + (double)LY;
+  SYNC();
+  chol_solve_reg<float, TB_MAXR>(R, w.bc(), n, grest, xr);
+  // ---- back substitution: the coupled positions and the belt from the dense solve, the singles on their lanes
+  const float xb = xr[m];
+  for (int i = LANE; i < m; i += WAVE) dir[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] = xr[i];
+  if (LANE == 0) dir[0] = xb;
+  if (single) {
+    float x[9];
+#pragma unroll
+    for (int i = 8; i >= 0; i--) {
+      float a = y[i] - lb[i] * xb;
+#pragma unroll
+      for (int k = i + 1; k < 9; k++) a -= Lb[P9(k, i)] * x[k];
+      x[i] = a * dv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++)
+      if (i < (cube ? 6 : 9)) dir[d0 + i] = x[i];
+  }
+  SYNC();
+  return true;
+}
+
 template <typename T, typename DIM>
 __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, int arena, int64_t* ctr) {
   const DIM dm(M.dm);
@@ -4171,6 +4489,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     SPLITMARK(2, PH_CHDIAG);
     if (scatter)
       gather_JtF_sc(M, w, ncon, nrow, g, tmp);
+    else if (pc_scene<T, DIM>() && !(M.dbg_flags & 64))
+      gather_JtF_pc(M, w, ncon, nrow, g, tmp);
     else
       gather_JtF(M, w, ncon, nrow, g, false);
     SYNC();
@@ -4191,6 +4511,12 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
         contact_K(w, ncon);
         SYNC();
         chol_arrow_rl<T, DIM, true>(M, w, H, g, dir, ncon, nrow);
+        PMARK(PH_NCHOL);
+        solved = true;
+      }
+    }
+    if constexpr (treeblk_scene<T, DIM>()) {
+      if (!solved && !(M.dbg_flags & (2048 | 3)) && newton_treeblk<DIM>(M, w, g, dir, ncon, nrow)) {
         PMARK(PH_NCHOL);
         solved = true;
       }
@@ -4478,6 +4804,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   SYNC();
   if (scatter)
     gather_JtF_sc(M, w, ncon, nrow, w.fc(), tmp);
+  else if (pc_scene<T, DIM>() && !(M.dbg_flags & 64))
+    gather_JtF_pc(M, w, ncon, nrow, w.fc(), tmp);
   else
     gather_JtF(M, w, ncon, nrow, w.fc(), false);
   SYNC();

@@ -5,8 +5,10 @@ live handle, FactoryVecEnv.set_experiment):
   substep (FM_NO_MIDCACHE=1): the contact set is the same by construction, so the trajectories are bit-identical;
 * the wave-parallel box-box narrowphase (SAT axes and clipping candidates over 16 lanes per pair) against one lane per
   pair (FM_SERIAL_BOXBOX=1): the same arithmetic per axis / candidate, bit-identical in fp32 (fp64: to rounding);
-* the dense blocked matrix-core Cholesky of the (4,16) scene against the sparse LDS one (FM_CHOL_LDS=2): the same
-  factorisation up to float32 rounding order, so one env-step from the same state agrees to the SURVEY gate."""
+* the (4,16) scene's tree-block Newton solve (single trees factored per lane, the coupled trees + belt as one small
+  dense system) against the dense blocked matrix-core Cholesky of the whole Hessian (FM_NO_TREEBLK=1) and against the
+  sparse LDS one (FM_CHOL_LDS=2): the same factorisation up to float32 rounding order, so one env-step from the same
+  state agrees to the SURVEY gate."""
 import os
 import sys
 
@@ -76,7 +78,8 @@ def test_parallel_box_box_fp64_to_rounding():
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-def test_dense_cholesky_agrees_with_sparse_4x16():
+@pytest.mark.parametrize("other", ["FM_NO_TREEBLK=1", "FM_CHOL_LDS=2"])
+def test_treeblock_solve_agrees_with_dense_and_sparse_4x16(other):
     import parity_util as pu
     from factory_marl_amd import state as st
 
@@ -96,8 +99,8 @@ def test_dense_cholesky_agrees_with_sparse_4x16():
     s0 = env.get_state()
     a = (torch.rand(n, A, device=env.device, generator=g) < 0.5).float()
     res = []
-    for mode in (None, "2"):
-        env.set_experiment(f"FM_CHOL_LDS={mode}" if mode else "")
+    for mode in ("", other):
+        env.set_experiment(mode)
         env.set_state(s0)
         env.step_tensors(a)
         env.sync()
@@ -110,7 +113,7 @@ def test_dense_cholesky_agrees_with_sparse_4x16():
         qd, vd = pu.state_err(A, K, da, db)
         errs.append(max(qd.max(), vd.max()))
     errs = np.array(errs)
-    print(f"dense vs sparse Cholesky, one env-step from 128 states: median {np.median(errs):.2e}, "
+    print(f"tree-block solve vs {other}, one env-step from 128 states: median {np.median(errs):.2e}, "
           f"within 1e-4 {np.mean(errs <= 1e-4):.1%}, worst {errs.max():.2e}")
     assert np.mean(errs <= 1e-4) >= 0.9 and np.median(errs) <= 1e-5
 
