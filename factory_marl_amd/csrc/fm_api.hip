@@ -222,7 +222,7 @@ static uint32_t read_experiment_flags() {
       {"FM_TWO_PASS_SETUP", '1', 256}, // the warmstart candidates in two row passes
       {"FM_FORCE_RERUN", '1', 512},    // (2,4): every env-step abandoned at its first stage and run by the wide kernel
       {"FM_NO_RERUN", '1', 1024},      // (2,4): contacts above 64 cut (counted), no wide rerun
-      {"FM_NO_TREEBLK", '1', 2048},    // (4,16) fp32: the dense Hessian + matrix-core factor on every substep
+      {"FM_NO_TREEBLK", '1', 2048},    // (2,8), (2,10), (4,16) fp32: the dense Hessian + factors on every substep
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {

@@ -242,7 +242,7 @@ struct Lay {
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int mcache, mpos;  // cached midphase: uint32 [mc_cap(nv)] hit list, T [ncb][3] body positions at the build
   int bposd, bRd;    // fp32 scenes with DIM::f64arms: double [A][10][3], [A][10][9] arm body poses (narrowphase)
-  int tblk;          // fp32 (4,16): the tree-block Newton solve's workspace (TB_* below; Newton-phase only)
+  int tblk;          // fp32 (2,8), (2,10), (4,16): the tree-block Newton solve's workspace (TB_*; Newton phase)
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -503,7 +503,7 @@ __host__ __device__ constexpr int hstride(int tsize, int nv) { return (tsize == 
 // scratch floats after the padded Hessian (the dense Cholesky's inverse diagonal block)
 __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4 && nv > 80) ? 256 : 0; }
 
-// workspace of the tree-block Newton solve (fp32 (4,16)): per tree a 9 x 9 lower-triangle block (packed, P9) and its
+// workspace of the tree-block Newton solve (fp32 (2,8), (2,10), (4,16)): per tree a 9 x 9 lower-triangle block (packed, P9) and its
 // belt row, then the coupled trees' dense system (<= TB_MAXR positions incl. the belt, row stride = its size) and its
 // position -> (tree, local dof) map
 constexpr int TB_BLK = 54, TB_MAXR = 32;
@@ -659,9 +659,10 @@ struct FixedDims {
   // the (4,16) scene also keeps its midphase hit list and float64 arm poses in the global block: 50.0 -> 37.9 KB of
   // LDS, four arenas per CU instead of three
   static constexpr bool gl_lists = spill && A_ == 4 && K_ == 16 && FM_GL_LISTS;
-  // the fp32 (4,16) scene solves the Newton system tree block by tree block (newton_treeblk): its dense 133-dof
-  // Hessian in the global block is only the fallback for more than TB_MAXR coupled positions
-  static constexpr bool treeblk = A_ == 4 && K_ == 16 && FM_TREEBLK;
+  // the fp32 scenes with spilled records other than (2,4) solve the Newton system tree block by tree block
+  // (newton_treeblk): their dense Hessian in the global block is only the fallback for more than TB_MAXR coupled
+  // positions
+  static constexpr bool treeblk = spill && !(A_ == 2 && K_ == 4) && FM_TREEBLK;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class

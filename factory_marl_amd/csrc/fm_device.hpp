@@ -4098,7 +4098,8 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
 }
 
 // ------------------------------------------------------------------------------------------------
-// Tree-block Newton solve of the fp32 (4,16) scene (config 5): H dir = -g without the dense 133-dof Hessian.
+// Tree-block Newton solve of the fp32 scenes with spilled records ((2,8), (2,10): configs 3 / 4; (4,16): config 5):
+// H dir = -g without the dense Hessian.
 // H couples two trees only through a contact between them (mass matrix: belt scalar, cubes diagonal, arm 9 x 9
 // blocks; generic rows stay inside one arm).  Elimination order: the single trees (no contact with another moving
 // tree except the belt), then the coupled trees, the belt last.  In that order H is block diagonal over the singles
@@ -4115,8 +4116,9 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
 // tree -- the tree's own block) by LDS atomics; one lane per generic row likewise.  The same terms as the dense
 // assembly, summed in another order (fp32 rounding differs from the dense path; both are held to the oracle).
 // Returns false (nothing written but K_c) when more than TB_MAXR positions are coupled or a generic row couples two
-// trees: the caller runs the dense blocked factor.  Replaces the dense assembly + chol_dense_mfma, whose Hessian
-// lives in the arena's global block (round-4 phase profile: 44 + 117 us of 273 us per arena-substep).
+// trees: the caller runs the scene's dense path.  Replaces the dense assembly (global atomics: the Hessian lives in
+// the arena's global block) and the dense factors: (4,16) Hessian + Cholesky 44 + 117 -> 16 + 15 us of 273 -> 138 us
+// per arena-substep (round 4, profiles/r04h_phase_fp32_4x16_treeblk.json).
 // gather_JtF by per-contact scatter (the compile-time scenes whose contact records live in the arena's global block:
 // (2,8), (2,10), (4,16)): one lane per contact adds its <= 18 column products J_c' f_c into the float64 accumulator by
 // LDS atomics, one lane per generic row likewise -- one round of record loads for up to 64 contacts, where the per-dof

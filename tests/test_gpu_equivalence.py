@@ -118,9 +118,10 @@ def test_treeblock_solve_agrees_with_dense_and_sparse_4x16(other):
     assert np.mean(errs <= 1e-4) >= 0.9 and np.median(errs) <= 1e-5
 
 
-def _one_step(A, K, n, pre, switch, value="1", precision="fp32"):
+def _one_step(A, K, n, pre, switch, value="1", precision="fp32", base=""):
     """`pre` random-action env-steps from reset (n arenas of their own seeds: diverse states), then one env-step from
-    that record with the switch off and on; returns the per-arena worst relative state difference (SURVEY metric)"""
+    that record with the switch off and on (on top of the `base` switches); returns the per-arena worst relative state
+    difference (SURVEY metric)"""
     import parity_util as pu
     from factory_marl_amd import FactoryVecEnv
     from factory_marl_amd import state as st
@@ -138,7 +139,7 @@ def _one_step(A, K, n, pre, switch, value="1", precision="fp32"):
     a = torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1
     res = []
     for on in (False, True):
-        env.set_experiment(f"{switch}={value}" if on else "")
+        env.set_experiment(f"{base} {switch}={value}" if on else base)
         env.set_state(s0)
         env.step_tensors(a)
         env.sync()
@@ -152,10 +153,11 @@ def _one_step(A, K, n, pre, switch, value="1", precision="fp32"):
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 @pytest.mark.parametrize("A,K", [(2, 8), (2, 10)])
 def test_two_pass_arrowhead_agrees_with_bordered_factor(A, K):
-    """fp32 (2,8) / (2,10): the two-pass arrowhead block factor (chol_arrow2_rl, the default on arrowhead substeps)
-    against the bordered register + matrix-core Schur factor (FM_NO_ARROW=1) -- the same Cholesky of the same
-    Hessian in another summation order: one env-step from 256 diverse states agrees to float32 rounding"""
-    errs = _one_step(A, K, 256, 60, "FM_NO_ARROW")
+    """fp32 (2,8) / (2,10), dense-Hessian path (FM_NO_TREEBLK=1): the two-pass arrowhead block factor (chol_arrow2_rl,
+    that path's default on arrowhead substeps) against the bordered register + matrix-core Schur factor
+    (FM_NO_ARROW=1) -- the same Cholesky of the same Hessian in another summation order: one env-step from 256 diverse
+    states agrees to float32 rounding"""
+    errs = _one_step(A, K, 256, 60, "FM_NO_ARROW", base="FM_NO_TREEBLK=1")
     print(f"({A},{K}) two-pass arrowhead vs bordered factor, one env-step from 256 states: median {np.median(errs):.2e}, "
           f"99th pct {np.quantile(errs, 0.99):.2e}, worst {errs.max():.2e}")
     assert np.median(errs) <= 1e-6 and np.mean(errs <= 1e-5) >= 0.99 and errs.max() <= 1e-4
@@ -169,3 +171,14 @@ def test_one_pass_warmstart_products_are_exact(precision):
     a, b = _run(2, 4, 256, 40, "FM_TWO_PASS_SETUP", precision=precision)
     assert np.array_equal(a, b)
 
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("A,K", [(2, 8), (2, 10)])
+def test_treeblock_solve_agrees_with_dense_path(A, K):
+    """fp32 (2,8) / (2,10): the tree-block Newton solve (the default) against the dense global-block Hessian with its
+    arrowhead / bordered factors (FM_NO_TREEBLK=1) -- the same system in another summation order"""
+    errs = _one_step(A, K, 256, 60, "FM_NO_TREEBLK")
+    print(f"({A},{K}) tree-block vs dense path, one env-step from 256 states: median {np.median(errs):.2e}, "
+          f"99th pct {np.quantile(errs, 0.99):.2e}, worst {errs.max():.2e}")
+    assert np.median(errs) <= 1e-6 and np.mean(errs <= 1e-5) >= 0.99 and errs.max() <= 1e-4
