@@ -64,7 +64,7 @@ EXPORTED = [
     "fm_config_default", "fm_create", "fm_destroy", "fm_last_error", "fm_set_stream", "fm_sync", "fm_obs_dim",
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
     "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile", "fm_scene_mjcf",
-    "fm_render", "fm_render_ngeom", "fm_set_param", "fm_get_param", "fm_num_counters",
+    "fm_render", "fm_render_ngeom", "fm_set_param", "fm_get_param", "fm_num_counters", "fm_get_costs",
 ]
 
 _LIB = None
@@ -108,6 +108,8 @@ def load():
     L.fm_set_state.restype = I
     L.fm_get_counters.argtypes = [P, P]
     L.fm_get_counters.restype = I
+    L.fm_get_costs.argtypes = [P, P]
+    L.fm_get_costs.restype = I
     L.fm_debug_dump.argtypes = [P, I, I, P, I]
     L.fm_debug_dump.restype = I
     L.fm_profile.argtypes = [P, I, P]

@@ -222,6 +222,7 @@ static uint32_t read_experiment_flags() {
       {"FM_TWO_PASS_SETUP", '1', 256}, // the warmstart candidates in two row passes
       {"FM_FORCE_RERUN", '1', 512},    // (2,4): every env-step abandoned at its first stage and run by the wide kernel
       {"FM_NO_RERUN", '1', 1024},      // (2,4): contacts above 64 cut (counted), no wide rerun
+      {"FM_PC_SCATTER", '1', 4096},    // (2,4): J' f by the per-contact scatter instead of per (contact, column)
       {"FM_NO_TREEBLK", '1', 2048},    // (2,8), (2,10), (4,16) fp32: the dense Hessian + factors on every substep
   };
   uint32_t f = 0;
@@ -1014,6 +1015,15 @@ int fm_get_counters(fm_handle* h, int64_t* host_out) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * FM_NCTR * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return FM_OK;
+}
+
+int fm_get_costs(fm_handle* h, uint32_t* host_out) {
+  if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
+  if (!h->cost) return set_err(FM_EINVAL, "no per-arena costs (FACTORYSIM_NO_LPT)");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(host_out, h->cost, (size_t)h->dm.N * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return FM_OK;
 }
 

@@ -662,7 +662,9 @@ struct FixedDims {
   // the fp32 scenes with spilled records other than (2,4) solve the Newton system tree block by tree block
   // (newton_treeblk): their dense Hessian in the global block is only the fallback for more than TB_MAXR coupled
   // positions
-  static constexpr bool treeblk = spill && !(A_ == 2 && K_ == 4) && FM_TREEBLK;
+  // (and so does the (2,4) scene's wide rerun kernel: its stages hold 65-128 contacts, where the dense register
+  // factor's per-pivot LDS broadcasts cost ~25 ms for one arena's env-step)
+  static constexpr bool treeblk = (WIDE_ || (spill && !(A_ == 2 && K_ == 4))) && FM_TREEBLK;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class

@@ -4159,7 +4159,7 @@ __device__ __forceinline__ void gather_JtF_pc(const Model<T>& M, const Ws<T, DIM
 template <typename T, typename DIM>
 __device__ constexpr bool pc_scene() {
   if constexpr (DIM::fixed)
-    return DIM::spill && !(DIM::MAXC == WAVE && DIM::nv <= 48);  // not the (2,4) scene (its own scatter)
+    return (DIM::spill || DIM::rerun) && !(DIM::MAXC == WAVE && DIM::nv <= 48);  // not the (2,4) 64-contact scene
   else
     return false;
 }
@@ -4489,9 +4489,9 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     contact_f3(w, ncon);
     SYNC();
     SPLITMARK(2, PH_CHDIAG);
-    if (scatter)
+    if (scatter && !(M.dbg_flags & 4096))
       gather_JtF_sc(M, w, ncon, nrow, g, tmp);
-    else if (pc_scene<T, DIM>() && !(M.dbg_flags & 64))
+    else if ((pc_scene<T, DIM>() || scatter) && !(M.dbg_flags & 64))
       gather_JtF_pc(M, w, ncon, nrow, g, tmp);
     else
       gather_JtF(M, w, ncon, nrow, g, false);
@@ -4804,9 +4804,9 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   // final constraint forces at a
   contact_f3(w, ncon);
   SYNC();
-  if (scatter)
+  if (scatter && !(M.dbg_flags & 4096))
     gather_JtF_sc(M, w, ncon, nrow, w.fc(), tmp);
-  else if (pc_scene<T, DIM>() && !(M.dbg_flags & 64))
+  else if ((pc_scene<T, DIM>() || scatter) && !(M.dbg_flags & 64))
     gather_JtF_pc(M, w, ncon, nrow, w.fc(), tmp);
   else
     gather_JtF(M, w, ncon, nrow, w.fc(), false);

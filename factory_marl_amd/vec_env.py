@@ -42,7 +42,8 @@ TOGGLE_CLASSES = envs.TOGGLE_CLASSES
 EXPERIMENT_FLAGS = {("FM_CHOL_LDS", "1"): 1, ("FM_CHOL_LDS", "2"): 2, ("FM_SERIAL_BOXBOX", "1"): 4,
                     ("FM_NO_MIDCACHE", "1"): 8, ("FM_NO_ARROW", "1"): 16, ("FM_NO_ARROW", "2"): 32,
                     ("FM_NO_SCATTER", "1"): 64, ("FM_SERIAL_FK", "1"): 128, ("FM_TWO_PASS_SETUP", "1"): 256,
-                    ("FM_FORCE_RERUN", "1"): 512, ("FM_NO_RERUN", "1"): 1024, ("FM_NO_TREEBLK", "1"): 2048}
+                    ("FM_FORCE_RERUN", "1"): 512, ("FM_NO_RERUN", "1"): 1024, ("FM_NO_TREEBLK", "1"): 2048,
+                    ("FM_PC_SCATTER", "1"): 4096}
 
 # global scalars of the handle (fm_set_param), per-arena values of the state record, fixed at creation
 RUNTIME_PARAMS = ("pt_time", "initial_conveyor_speed", "conveyor_acceleration", "force_contact_threshold",
@@ -473,6 +474,14 @@ class FactoryVecEnv:
         self._bind_stream()
         out = np.zeros((self.num_envs, _lib.num_counters(self._L)), np.int64)
         _lib.check(self._L.fm_get_counters(self._h, out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def costs(self):
+        """diagnostic: each arena's last env-step duration in GPU wall-clock ticks (fm_get_costs; the longest-first
+        dispatch order is sorted by these)"""
+        self._bind_stream()
+        out = np.zeros(self.num_envs, np.uint32)
+        _lib.check(self._L.fm_get_costs(self._h, out.ctypes.data_as(C.c_void_p)))
         return out
 
     PHASES = ["fk", "geoms_mass", "collision", "rows", "smooth_acc", "newton_setup", "newton_grad",

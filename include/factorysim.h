@@ -155,6 +155,9 @@ int fm_set_state(fm_handle* h, const void* host_in);
  * [1] [2] then include the abandoned part of the step). */
 int fm_get_counters(fm_handle* h, int64_t* host_out);
 int fm_num_counters(void);
+/* Diagnostic: each arena's last env-step duration in GPU wall-clock ticks (host [N] uint32; 0 until its first step;
+ * the longest-first dispatch order of the next step is sorted by these) -- the launch's load balance. */
+int fm_get_costs(fm_handle* h, uint32_t* host_out);
 
 /* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [24] uint64).
  * mode 1 = zero and enable, 0 = disable, -1 = leave as is; host_out (may be NULL) receives the
