@@ -642,6 +642,9 @@ struct DimsSpill : Dims {
 #ifndef FM_TREEBLK
 #define FM_TREEBLK 1
 #endif
+#ifndef FM_TREEBLK_24
+#define FM_TREEBLK_24 0  // experiment builds: the (2,4) kernel with the tree-block solve (FM_TREEBLK_ONLY=1 selects it)
+#endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
@@ -664,7 +667,8 @@ struct FixedDims {
   // positions
   // (and so does the (2,4) scene's wide rerun kernel: its stages hold 65-128 contacts, where the dense register
   // factor's per-pivot LDS broadcasts cost ~25 ms for one arena's env-step)
-  static constexpr bool treeblk = (WIDE_ || (spill && !(A_ == 2 && K_ == 4))) && FM_TREEBLK;
+  static constexpr bool treeblk = (WIDE_ || (spill && !(A_ == 2 && K_ == 4)) || (A_ == 2 && K_ == 4 && FM_TREEBLK_24)) &&
+                                  FM_TREEBLK;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
