@@ -222,10 +222,8 @@ static uint32_t read_experiment_flags() {
       {"FM_TWO_PASS_SETUP", '1', 256}, // the warmstart candidates in two row passes
       {"FM_FORCE_RERUN", '1', 512},    // (2,4): every env-step abandoned at its first stage and run by the wide kernel
       {"FM_NO_RERUN", '1', 1024},      // (2,4): contacts above 64 cut (counted), no wide rerun
+      {"FM_NO_TREEBLK", '1', 2048},    // (2,8), (2,10), (4,16) fp32, wide rerun: the dense Hessian + factors on every substep
       {"FM_PC_SCATTER", '1', 4096},    // (2,4): J' f by the per-contact scatter instead of per (contact, column)
-      {"FM_NO_TREEBLK", '1', 2048},
-      {"FM_TREEBLK_ONLY", '1', 8192},
-      {"FM_HEAVY_TB", '1', 16384},     // (2,4) builds with FM_TREEBLK_24: tree-block solve / per-contact J'f on heavy substeps  // (2,4) builds with FM_TREEBLK_24: the tree-block solve on arrowhead substeps too    // (2,8), (2,10), (4,16) fp32: the dense Hessian + factors on every substep
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {

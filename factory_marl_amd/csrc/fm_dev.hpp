@@ -642,9 +642,6 @@ struct DimsSpill : Dims {
 #ifndef FM_TREEBLK
 #define FM_TREEBLK 1
 #endif
-#ifndef FM_TREEBLK_24
-#define FM_TREEBLK_24 0  // experiment builds: the (2,4) kernel with the tree-block solve (FM_TREEBLK_ONLY=1 selects it)
-#endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
@@ -667,8 +664,10 @@ struct FixedDims {
   // positions
   // (and so does the (2,4) scene's wide rerun kernel: its stages hold 65-128 contacts, where the dense register
   // factor's per-pivot LDS broadcasts cost ~25 ms for one arena's env-step)
-  static constexpr bool treeblk = (WIDE_ || (spill && !(A_ == 2 && K_ == 4)) || (A_ == 2 && K_ == 4 && FM_TREEBLK_24)) &&
-                                  FM_TREEBLK;
+  // (the (2,4) 64-contact kernel keeps its arrowhead register factor: with the tree-block code compiled in, round 4
+  // measured 175.8k vs 189.5k env-steps/s -- the extra code alone costs its register allocation -- and neither the
+  // tree-block solve on every substep nor only on heavy substeps (> 8 contacts on a tree) won that back)
+  static constexpr bool treeblk = (WIDE_ || (spill && !(A_ == 2 && K_ == 4))) && FM_TREEBLK;
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class

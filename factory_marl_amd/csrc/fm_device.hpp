@@ -35,12 +35,6 @@
 #include "fm_arm_table.hpp"  // generated (gen_tables.cpp)
 #include "fm_ik.hpp"
 
-#ifndef FM_TB_HEAVY
-#define FM_TB_HEAVY 8
-#endif
-#ifndef FM_PC_HEAVY
-#define FM_PC_HEAVY 24
-#endif
 #ifndef FM_WS_RUNTIME_LAYOUT
 #define FM_WS_RUNTIME_LAYOUT 0
 #endif
@@ -4489,25 +4483,13 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   int it;
   const int maxit = M.solver_iter;
   const bool scatter = arrow_scene<T, DIM>() && !(M.dbg_flags & 64);  // gather_JtF_sc (FM_NO_SCATTER=1: off)
-  // heavy substeps of the (2,4) scene (cubes in a pile: a tree with more than FM_TB_HEAVY contacts -- the arenas
-  // whose env-steps run 2-3x the mean and end the launch, profiles/r04o_*): the tree-block solve (one lane per
-  // contact) instead of the arrowhead factor's per-lane walks over a tree's contacts, and above FM_PC_HEAVY contacts
-  // the per-contact J'f scatter instead of the per-(contact, column) rounds (switch 16384, FM_HEAVY_TB=1)
-  bool heavy = false, heavy_pc = false;
-  if constexpr (arrow_scene<T, DIM>() && treeblk_scene<T, DIM>()) {
-    if (M.dbg_flags & 16384) {
-      const int mc = (LANE >= 1 && LANE < DIM::ntree) ? __popcll(w.tmask()[LANE]) : 0;
-      heavy = wave_max(mc) > FM_TB_HEAVY;
-      heavy_pc = ncon > FM_PC_HEAVY;
-    }
-  }
   const int ntri = nv * (nv + 1) / 2;
   for (it = 0; it < maxit; it++) {
     // gradient g = M(a - as) + J' D jar (active)
     contact_f3(w, ncon);
     SYNC();
     SPLITMARK(2, PH_CHDIAG);
-    if (scatter && !(M.dbg_flags & 4096) && !heavy_pc)
+    if (scatter && !(M.dbg_flags & 4096))
       gather_JtF_sc(M, w, ncon, nrow, g, tmp);
     else if ((pc_scene<T, DIM>() || scatter) && !(M.dbg_flags & 64))
       gather_JtF_pc(M, w, ncon, nrow, g, tmp);
@@ -4527,7 +4509,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     // substep): H is assembled straight into the block-parallel factor's registers, no LDS Hessian
     bool solved = false;
     if constexpr (arrow_scene<T, DIM>()) {
-      if (!(M.dbg_flags & (32 | 8192)) && !heavy && arrow_substep(M, w)) {
+      if (!(M.dbg_flags & 32) && arrow_substep(M, w)) {
         contact_K(w, ncon);
         SYNC();
         chol_arrow_rl<T, DIM, true>(M, w, H, g, dir, ncon, nrow);
@@ -4822,7 +4804,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   // final constraint forces at a
   contact_f3(w, ncon);
   SYNC();
-  if (scatter && !(M.dbg_flags & 4096) && !heavy_pc)
+  if (scatter && !(M.dbg_flags & 4096))
     gather_JtF_sc(M, w, ncon, nrow, w.fc(), tmp);
   else if ((pc_scene<T, DIM>() || scatter) && !(M.dbg_flags & 64))
     gather_JtF_pc(M, w, ncon, nrow, w.fc(), tmp);
