@@ -16,7 +16,7 @@ reported under "diagnostics") instead of the first seconds of one synchronised e
 Roofline: the dominant (only) kernel in the timed region is fm::step_kernel; its average launch time is
 measured with HIP events on the stream it runs on.  Algorithmic bytes per arena env-step
 B(A,K) = 100*8*(nq + 2nv + nu) + 4*(act_dim + obs_dim + 4) = 120,480 B at (2,4).  The
-kernel is bound by neither HBM nor MFMA but by dependent LDS / VALU latency chains at one wave per SIMD;
+kernel is bound by neither HBM nor MFMA but by dependent LDS / VALU / L2 latency chains at two waves per SIMD;
 "roofline.valu" prices its VALU work (PMC instruction counts per arena env-step, profiles/) against the
 fp32 vector peak with the live kernel time.
 CPU baseline: the oracle (our C restatement of the reference algorithm, oracle/) stepped with OpenMP on
@@ -403,7 +403,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                 "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
                 "algorithmic_bytes_per_arena_step": B,
-                "binding": "neither HBM nor MFMA: dependent LDS/VALU latency chains, one wave (arena) per SIMD"}
+                "binding": "neither HBM nor MFMA: dependent LDS / VALU / L2 latency chains, two waves (arenas) per SIMD"}
+        if traffic is not None:
+            roof["traffic_note"] = ("PMC TCC -> memory-fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE): the per-arena "
+                                    "scratch blocks (contact records, Hessian) and register spills that leave the L2, "
+                                    "whether the MALL or HBM serves them; %.1f %% of the HBM peak at this launch time"
+                                    % (100.0 * traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS))
         vj = load_json(args.valu_json) or {}
         if vj.get("A") == A and vj.get("K") == K and vj.get("precision") == args.precision:
             flops = vj["valu_lane_flops_per_arena_step"] * N
