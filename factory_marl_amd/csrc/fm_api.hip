@@ -224,6 +224,7 @@ static uint32_t read_experiment_flags() {
       {"FM_NO_RERUN", '1', 1024},      // (2,4): contacts above 64 cut (counted), no wide rerun
       {"FM_NO_TREEBLK", '1', 2048},    // (2,8), (2,10), (4,16) fp32, wide rerun: the dense Hessian + factors on every substep
       {"FM_PC_SCATTER", '1', 4096},    // (2,4): J' f by the per-contact scatter instead of per (contact, column)
+      {"FM_TB_LDSBC", '1', 8192},      // tree-block solve: its coupled system by the LDS-broadcast register factor
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {

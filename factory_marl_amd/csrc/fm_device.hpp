@@ -3862,6 +3862,59 @@ __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const 
   SYNC();
 }
 
+// chol_solve_reg for the tree-block solve's small coupled system (fp32, n <= NVM): the same factor, but the pivot
+// column reaches the other lanes by v_readlane (lane i holds L[i][k] after the scaling) instead of an LDS row and two
+// wave barriers per pivot -- the system is one small dense block solved once per Newton iteration
+template <int NVM>
+__device__ __forceinline__ void chol_solve_rl(const float* H, int nv, const double* g, float* dir) {
+  const int j = LANE;
+  const float tiny = 1e-37f;
+  float col[NVM];
+#pragma unroll
+  for (int i = 0; i < NVM; i++) col[i] = (i < nv && j < nv) ? H[i * nv + j] : 0.0f;
+  SYNC();
+  float dinv = 1.0f;
+#pragma unroll
+  for (int k = 0; k < NVM; k++) {
+    if (k < nv) {
+      float d = readlane(col[k], k);
+      d = d > tiny ? d : tiny;
+      const float ri = 1.0f / sqrtf(d);
+      const float lj = col[k] * ri;  // lane j > k: L[j][k]; lane k: L[k][k]
+      if (j == k) dinv = ri;
+      if (j >= k) col[k] = lj;
+      float lv[NVM];
+#pragma unroll
+      for (int i = k + 1; i < NVM; i++) lv[i] = readlane(lj, i);
+      if (j > k) {
+#pragma unroll
+        for (int i = k + 1; i < NVM; i++) col[i] -= lv[i] * lj;
+      }
+    }
+  }
+  float acc = j < nv ? (float)-g[j] : 0.0f;
+  float y = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NVM; k++) {
+    if (k < nv) {
+      const float yk = readlane(acc * dinv, k);
+      if (j == k) y = yk;
+      if (j > k) acc -= col[k] * yk;
+    }
+  }
+  float acc2 = y, x = 0.0f;
+#pragma unroll
+  for (int k = NVM - 1; k >= 0; k--) {
+    if (k < nv) {
+      const float xk = readlane(acc2 * dinv, k);
+      if (j == k) x = xk;
+      if (j < k) acc2 -= col[k] * dinv * xk;
+    }
+  }
+  if (j < nv) dir[j] = x;
+  SYNC();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Newton solver on the primal cost (see oracle/solver.c for the definition)
 // ------------------------------------------------------------------------------------------------
@@ -4109,7 +4162,7 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
 //  * the rest -- the coupled trees (an arm grasping a cube, two cubes touching: 15-24 dofs measured on the oracle's
 //    PauseIKToggle trajectories) plus the belt, with the singles' Schur terms sum l_t'l_t and sum l_t'y_t folded into
 //    the belt's diagonal and right-hand side -- is one small dense system for the register Cholesky
-//    (chol_solve_reg<float, TB_MAXR>);
+//    (chol_solve_rl<TB_MAXR>: pivots by v_readlane; FM_TB_LDSBC=1 the LDS-broadcast chol_solve_reg);
 //  * the singles' backward solves take the belt's solution from it.
 // The blocks are assembled in LDS (the Newton phase's share of the collision scratch): one lane per contact adds
 // B_a'K B_a, B_b'K B_b and the cross term B_a'K B_b (a belt row, the coupled system, or -- a contact inside one
@@ -4387,7 +4440,10 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
   for (int i = LANE; i < n; i += WAVE)
     grest[i] = i < m ? g[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] : g[0] + (double)LY;
   SYNC();
-  chol_solve_reg<float, TB_MAXR>(R, w.bc(), n, grest, xr);
+  if (M.dbg_flags & 8192)
+    chol_solve_reg<float, TB_MAXR>(R, w.bc(), n, grest, xr);
+  else
+    chol_solve_rl<TB_MAXR>(R, n, grest, xr);
   // ---- back substitution: the coupled positions and the belt from the dense solve, the singles on their lanes
   const float xb = xr[m];
   for (int i = LANE; i < m; i += WAVE) dir[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] = xr[i];
