@@ -4126,16 +4126,33 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
   const DIM dm(M.dm);
   for (int i = LANE; i < dm.nv; i += WAVE) acc[i] = 0.0;
   SYNC();
-  for (int e = LANE; e < CJ * ncon; e += WAVE) {
-    const int c = e / CJ, ii = e - CJ * c;
-    const int* ci = w.ci() + 4 * c;
-    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-    const T* cr = w.cr() + CR_N * c;
-    const T* J = cr + CR_J;
-    const double* f3 = dslot(cr, CR_F3);
-    const double v = (double)J[ii] * f3[0] + (double)J[CJ + ii] * f3[1] + (double)J[2 * CJ + ii] * f3[2];
-    const int gi = ii < nda ? tree_dof(dm, ta) + ii : tree_dof(dm, tb >= 0 ? tb : 0) + ii - nda;
-    if (ii < nda + ndb) atomicAdd(acc + gi, v);
+#ifndef FM_SC_UNROLL
+#define FM_SC_UNROLL 2
+#endif
+  // FM_SC_UNROLL rounds of (contact, column) pairs per pass: their record loads (the arena's global block) issue
+  // together before the atomics, in the same atomic order as one round per pass (round 4, one box, two runs each:
+  // config 2 187.8k -> 190.0k with 2 rounds, 184.3k with 4 -- the registers they hold, profiles/r04s_*)
+  for (int e0 = LANE; e0 < CJ * ncon; e0 += FM_SC_UNROLL * WAVE) {
+    double v[FM_SC_UNROLL];
+    int gi[FM_SC_UNROLL];
+    bool ok[FM_SC_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FM_SC_UNROLL; u++) {
+      const int e = e0 + u * WAVE;
+      const int c = e < CJ * ncon ? e / CJ : 0, ii = e < CJ * ncon ? e - CJ * c : CJ;
+      const int* ci = w.ci() + 4 * c;
+      const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+      const T* cr = w.cr() + CR_N * c;
+      const T* J = cr + CR_J;
+      const double* f3 = dslot(cr, CR_F3);
+      const int iic = ii < CJ ? ii : 0;
+      v[u] = (double)J[iic] * f3[0] + (double)J[CJ + iic] * f3[1] + (double)J[2 * CJ + iic] * f3[2];
+      gi[u] = ii < nda ? tree_dof(dm, ta) + ii : tree_dof(dm, tb >= 0 ? tb : 0) + ii - nda;
+      ok[u] = ii < nda + ndb;
+    }
+#pragma unroll
+    for (int u = 0; u < FM_SC_UNROLL; u++)
+      if (ok[u]) atomicAdd(acc + gi[u], v[u]);
   }
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;

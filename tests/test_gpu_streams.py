@@ -81,5 +81,12 @@ def test_longest_first_dispatch_does_not_change_results(monkeypatch):
     plain.sync()
     assert torch.equal(lpt.obs, plain.obs)
     assert np.array_equal(lpt.get_state(), plain.get_state())
+    # the durations the order is sorted by (fm_get_costs): every arena stepped, each env-step under a second
+    c = lpt.costs()
+    assert c.shape == (n,) and (c > 0).all() and (c < 100_000_000).all()  # 100 MHz wall clock ticks
+    from factory_marl_amd._lib import FactorySimError
+
+    with pytest.raises(FactorySimError):
+        plain.costs()  # FACTORYSIM_NO_LPT: no per-arena costs kept
     lpt.close()
     plain.close()
