@@ -65,6 +65,7 @@ EXPORTED = [
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
     "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile", "fm_scene_mjcf",
     "fm_render", "fm_render_ngeom", "fm_set_param", "fm_get_param", "fm_num_counters", "fm_get_costs",
+    "fm_kernel_timing", "fm_get_kernel_time",
 ]
 
 _LIB = None
@@ -110,6 +111,10 @@ def load():
     L.fm_get_counters.restype = I
     L.fm_get_costs.argtypes = [P, P]
     L.fm_get_costs.restype = I
+    L.fm_kernel_timing.argtypes = [P, I]
+    L.fm_kernel_timing.restype = I
+    L.fm_get_kernel_time.argtypes = [P, P, P]
+    L.fm_get_kernel_time.restype = I
     L.fm_debug_dump.argtypes = [P, I, I, P, I]
     L.fm_debug_dump.restype = I
     L.fm_profile.argtypes = [P, I, P]

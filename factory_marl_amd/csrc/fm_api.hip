@@ -108,6 +108,8 @@ struct fm_handle {
   char* bak = nullptr;
   Lay lay_rerun{};
   char* spill_buf = nullptr;   // [N][spill_stride]
+  bool ktime_on = false;                                   // fm_kernel_timing
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ktime;  // one event pair per step-kernel launch since the last read
   long long spill_stride = 0;  // Lay::gtotal of the spill layout in use (compile-time scenes; runtime fp64 (4,16))
 };
 
@@ -204,6 +206,7 @@ static Model<T> make_model(const fm_handle* h) {
 // experiment switches of the kernel (A/B probes and the equivalence tests; every default is 0): read from the
 // environment once, at fm_create, and reported on stderr when any is set; "experiment_flags" (fm_set_param) changes
 // them on a live handle for later launches
+constexpr uint32_t FM_XFLAGS_MASK = 0x3FFFu;  // the switches below (fm_set_param rejects other bits)
 static uint32_t read_experiment_flags() {
   struct Sw {
     const char* var;
@@ -583,11 +586,36 @@ static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik) {
   rerun_launch<T, 2, 4>(pr, h->dm.N, h->stream, ik);
 }
 
+// kernel-only timing (fm_kernel_timing): a HIP event pair on the handle's stream around each env-step kernel launch
+// -- the step kernel alone, without the dispatch-order kernel, the rerun-list reset or the wide rerun launch
+static void ktime_begin(fm_handle* h) {
+  if (!h->ktime_on) return;
+  hipEvent_t a = nullptr, b = nullptr;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+  (void)hipEventRecord(a, h->stream);
+  h->ktime.push_back({a, b});
+}
+static void ktime_end(fm_handle* h) {
+  if (h->ktime_on && !h->ktime.empty()) (void)hipEventRecord(h->ktime.back().second, h->stream);
+}
+static void ktime_clear(fm_handle* h) {
+  for (auto& e : h->ktime) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  h->ktime.clear();
+}
+
 template <typename T>
 static void launch_step(fm_handle* h, const StepIO& io) {
   if (h->order) hipLaunchKernelGGL(lpt_order_kernel, dim3(1), dim3(1024), 0, h->stream, h->cost, h->order, h->dm.N);
-  const bool rerun = h->rerun && !(h->xflags & 1024);
-  if (rerun) (void)hipMemsetAsync(h->rerun, 0, sizeof(int32_t), h->stream);
+  bool rerun = h->rerun && !(h->xflags & 1024);
+  if (rerun && hipMemsetAsync(h->rerun, 0, sizeof(int32_t), h->stream) != hipSuccess) {
+    // a stale count would make the rerun kernel re-step the previous launch's abandoned arenas: run without the
+    // rerun list instead (stages above 64 contacts are then cut and counted in counters[0])
+    fprintf(stderr, "factorysim: clearing the rerun list failed; this launch cuts contacts above 64\n");
+    rerun = false;
+  }
   const StepParams<T> pd{make_model<T>(h), make_state<T>(h), h->lay, io};
   dim3 grid(h->dm.N), block(WAVE);
   const bool ik = h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS;
@@ -601,7 +629,9 @@ static void launch_step(fm_handle* h, const StepIO& io) {
       pf.S.rerun = h->rerun;                                                                           \
       pf.S.bak = h->bak;                                                                               \
     }                                                                                                  \
+    ktime_begin(h);                                                                                    \
     fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream, ik);                              \
+    ktime_end(h);                                                                                      \
     if (rerun) launch_rerun<T>(h, pd, ik);                                                             \
     return;                                                                                            \
   }                                                                                                    \
@@ -612,12 +642,14 @@ static void launch_step(fm_handle* h, const StepIO& io) {
   }
 #undef X
   (void)idx;
+  ktime_begin(h);
   if constexpr (sizeof(T) == 8) {
     if (h->spill) {
       if (ik)
         hipLaunchKernelGGL((step_kernel<T, DimsSpill, true>), grid, block, h->lay.total, h->stream, pd);
       else
         hipLaunchKernelGGL((step_kernel<T, DimsSpill, false>), grid, block, h->lay.total, h->stream, pd);
+      ktime_end(h);
       return;
     }
   }
@@ -625,6 +657,7 @@ static void launch_step(fm_handle* h, const StepIO& io) {
     hipLaunchKernelGGL((step_kernel<T, Dims, true>), grid, block, h->lay.total, h->stream, pd);
   else
     hipLaunchKernelGGL((step_kernel<T, Dims, false>), grid, block, h->lay.total, h->stream, pd);
+  ktime_end(h);
 }
 
 // base colour of each collidable geom (assets/scene.xml, scene.py, conveyor_belt.xml, iiwa14.xml materials;
@@ -795,6 +828,7 @@ void fm_destroy(fm_handle* h) {
   // the arena state may still be in use by work queued on the current stream (the caller's or ours)
   (void)hipStreamSynchronize(h->stream);
   if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
+  ktime_clear(h);
   for (void* p : h->allocs) (void)hipFree(p);
   for (void* p : {(void*)h->render_rgb, (void*)h->cube_rgba, (void*)h->render_frames, (void*)h->render_arenas})
     if (p) (void)hipFree(p);
@@ -844,7 +878,8 @@ static double* param_slot(fm_handle* h, const char* name, double* scale) {
 int fm_set_param(fm_handle* h, const char* name, double value) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   if (name && std::string(name) == "experiment_flags") {
-    if (!(value >= 0 && value < 65536 && value == (double)(uint32_t)value)) return set_err(FM_EINVAL, "bad flags");
+    if (!(value >= 0 && value < 65536 && value == (double)(uint32_t)value) || ((uint32_t)value & ~FM_XFLAGS_MASK))
+      return set_err(FM_EINVAL, "bad flags: experiment switches are the bits of 0x3FFF (fm_api.hip read_experiment_flags)");
     h->xflags = (uint32_t)value;
     return FM_OK;
   }
@@ -1025,6 +1060,31 @@ int fm_get_costs(fm_handle* h, uint32_t* host_out) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(host_out, h->cost, (size_t)h->dm.N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return FM_OK;
+}
+
+int fm_kernel_timing(fm_handle* h, int enable) {
+  if (!h) return set_err(FM_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  ktime_clear(h);
+  h->ktime_on = enable != 0;
+  return FM_OK;
+}
+
+int fm_get_kernel_time(fm_handle* h, double* total_ms, int* launches) {
+  if (!h || !total_ms || !launches) return set_err(FM_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  double t = 0.0;
+  for (auto& e : h->ktime) {
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
+    t += ms;
+  }
+  *total_ms = t;
+  *launches = (int)h->ktime.size();
+  ktime_clear(h);
   return FM_OK;
 }
 

@@ -15,10 +15,16 @@ namespace fm {
 #if defined(__HIP_DEVICE_COMPILE__)
 #define FM_AS_CONST __attribute__((address_space(4)))
 #define FM_AS_GLOBAL __attribute__((address_space(1)))
+#define FM_AS(n) __attribute__((address_space(n)))
 #else
 #define FM_AS_CONST
 #define FM_AS_GLOBAL
+#define FM_AS(n)
 #endif
+// address spaces by number (FM_AS(n)): 1 global, 3 LDS, 4 constant.  Non-inlined device functions take their
+// pointer parameters in a named address space: a plain pointer parameter is generic inside the callee, and every
+// access through it a FLAT instruction (tests/test_build_flags.py asserts that no step kernel has one)
+enum { AS_GLOBAL = 1, AS_LDS = 3, AS_CONST = 4 };
 template <typename X>
 struct cptr {
   const X* p;
@@ -504,12 +510,16 @@ __host__ __device__ constexpr int hstride(int tsize, int nv) { return (tsize == 
 __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4 && nv > 80) ? 256 : 0; }
 
 // workspace of the tree-block Newton solve (fp32 (2,8), (2,10), (4,16)): per tree a 9 x 9 lower-triangle block (packed, P9) and its
-// belt row, then the coupled trees' dense system (<= TB_MAXR positions incl. the belt, row stride = its size) and its
-// position -> (tree, local dof) map
+// belt row, then the coupled trees' dense system (<= TB_MAXR positions incl. the belt, row stride = its size), its
+// position -> (tree, local dof) map, and the coupled system's right-hand side (TB_MAXR doubles) and solution
+// (TB_MAXR floats) -- their own slots: the solver's nv-double scratch w.tmp() is too small for them at (2,4)
+// (nv = 43 < 1.5 TB_MAXR)
 constexpr int TB_BLK = 54, TB_MAXR = 32;
 __host__ __device__ constexpr int tb_rest(int ntree) { return (TB_BLK * ntree + 3) & ~3; }
 __host__ __device__ constexpr int tb_map(int ntree) { return tb_rest(ntree) + TB_MAXR * TB_MAXR; }
-__host__ __device__ constexpr int tb_floats(int ntree) { return tb_map(ntree) + TB_MAXR; }
+__host__ __device__ constexpr int tb_rhs(int ntree) { return (tb_map(ntree) + TB_MAXR + 3) & ~3; }  // 16-byte aligned
+__host__ __device__ constexpr int tb_sol(int ntree) { return tb_rhs(ntree) + 2 * TB_MAXR; }
+__host__ __device__ constexpr int tb_floats(int ntree) { return tb_sol(ntree) + TB_MAXR; }
 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,

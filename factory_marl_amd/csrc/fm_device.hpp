@@ -1487,7 +1487,11 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // DIM::midcache: the list of an inflated test (every bound + MC_MARGIN) is kept and reused while no moving
   // body has moved MC_HALF since it was built -- a pair outside the inflated test then cannot pass the exact one,
   // and the geom-pair test and narrowphase below decide the contacts as before (so the contact set is unchanged)
-  uint32_t* sp = w.sp();
+  // the list is built in w.sp() (the arena's global block with DIM::gl_lists, else LDS) and read back from there or,
+  // when the cached list is reused, from w.mcache() (LDS): reads go through address-space-typed pointers chosen per
+  // access, never through one pointer selected between the two (that would be generic: FLAT instructions)
+  uint32_t* const sp = w.sp();
+  constexpr int SPAS = DIM::gl_lists ? AS_GLOBAL : AS_LDS;
   int nsp = 0, total = 0;
   bool reuse = false;
   T infl = T(0);
@@ -1503,7 +1507,6 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     }
     reuse = ok && __ballot(moved) == 0ull;
     if (reuse) {
-      sp = w.mcache();
       nsp = misc[MISC_MC_N];
       total = misc[MISC_MC_TOT];
     } else {
@@ -1531,7 +1534,9 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     const int ncomb = hit ? n1 * n2 : 0;
     const uint64_t bal = __ballot(hit);
     const int incl = wave_incl_scan(ncomb);
-    if (hit) sp[nsp + __popcll(bal & below)] = (bpw & 0xFFFFu) | ((uint32_t)(total + incl - ncomb) << 16);
+    if (hit)
+      ((uint32_t FM_AS(SPAS)*)sp)[nsp + __popcll(bal & below)] =
+          (bpw & 0xFFFFu) | ((uint32_t)(total + incl - ncomb) << 16);
     nsp += __popcll(bal);
     total += __builtin_amdgcn_readlane(incl, WAVE - 1);
   };
@@ -1543,7 +1548,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
       if constexpr (DIM::midcache) {
         // keep the inflated list (when it fits) and the positions it was built at
         const bool fits = nsp <= mc_cap(DIM::nv);
-        for (int e = LANE; e < nsp && fits; e += WAVE) w.mcache()[e] = sp[e];
+        for (int e = LANE; e < nsp && fits; e += WAVE) w.mcache()[e] = ((const uint32_t FM_AS(SPAS)*)sp)[e];
         for (int b = LANE; b < dm.ncb; b += WAVE) {
           const T* o = w.cbw() + 8 * b;
           T* p0 = w.mpos() + 3 * b;
@@ -1582,6 +1587,10 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // increasing: every hit pair expands to >= 1 geom pair), and the pass's last owner carries into the next
   int* mark = misc + 16;  // [64] scratch of the collision phase
   int carry = 0;
+  auto sp_at = [&](int i) -> uint32_t {
+    if (DIM::midcache && reuse) return ((const uint32_t FM_AS(AS_LDS)*)w.mcache())[i];
+    return ((const uint32_t FM_AS(SPAS)*)sp)[i];
+  };
   for (int e0 = 0; e0 < total; e0 += WAVE) {
     const int e = e0 + LANE;
     bool ok = false;
@@ -1590,7 +1599,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     mark[LANE] = -1;
     SYNC();
     for (int q = LANE; q < nsp; q += WAVE) {
-      const int st = (int)(sp[q] >> 16);
+      const int st = (int)(sp_at(q) >> 16);
       if (st >= e0 && st < e0 + WAVE) mark[st - e0] = q;
     }
     SYNC();
@@ -1598,7 +1607,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
     own = own > carry ? own : carry;
     carry = __builtin_amdgcn_readlane(own, WAVE - 1);
     if (e < total) {
-      const uint32_t bp = sp[own];
+      const uint32_t bp = sp_at(own);
       const int x = bp & 255, y = (bp >> 8) & 255;
       const int r = e - (int)(bp >> 16);
       const int ngy = cbi[4 * y + 3];
@@ -2707,10 +2716,13 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
 // ------------------------------------------------------------------------------------------------
 template <typename T, typename DIM>
 __device__ __forceinline__ T Mdiag(const Model<T>& M, const Ws<T, DIM>& w, int i) {
-  if (i == 0) return M.belt_mass;
-  int k = (i - 1) / 6, r = (i - 1) % 6;
-  const T* c = w.cube() + 4 * k;
-  return r < 3 ? c[1] : c[2];
+  // both loads unconditional and the select on the values: with `if (i == 0) return M.belt_mass;` the compiler
+  // merged the kernarg load and the LDS load into one load through a selected generic pointer (a FLAT instruction,
+  // tools/isa_flat.py)
+  const T bm = M.belt_mass;
+  const int ii = i > 0 ? i - 1 : 0, k = ii / 6, r = ii - 6 * k;
+  const T cv = w.cube()[4 * k + (r < 3 ? 1 : 2)];
+  return i == 0 ? bm : cv;
 }
 
 // out = M x   (lanes over dofs), accumulated in out's type (the solver's float64 vectors: M's float entries
@@ -3928,31 +3940,57 @@ __device__ __forceinline__ T edge_val(const T* x3, T mu, int e) {
 // contact's own are selected away, never multiplied), accumulated in O and stored as O at the record's slot
 // (O = T for the velocity products of the rows' reference accelerations; O = double for the Newton iterate's
 // products JA / JD, whose float-by-float terms are exact in double)
+#ifndef FM_JX_UNROLL
+#define FM_JX_UNROLL 2
+#endif
+// rounds of (contact, row) items per pass of contact_jx / rows_eval2 in the scenes whose contact capacity exceeds the
+// wave (their records live in the arena's global scratch block: the rounds' record loads issue together).  A round
+// past the last item reads record 0 (always valid when the loop runs) and stores nothing: no load indexes a slot at
+// or beyond ncon, whose records hold stale data of an earlier stage.
+template <typename DIM>
+__host__ __device__ constexpr int jx_rounds() {
+  return DIM::MAXC > WAVE ? FM_JX_UNROLL : 1;
+}
 template <typename O, typename T, typename DIM, typename X>
 __device__ __forceinline__ void contact_jx(const Model<T>& M, const Ws<T, DIM>& w, const X* x, int ncon, int slot) {
   const DIM dm(M.dm);
-  for (int e = LANE; e < 3 * ncon; e += WAVE) {
-    const int c = e / 3, r = e - 3 * c;
-    const int* ci = w.ci() + 4 * c;
-    T* cr = w.cr() + CR_N * c;
-    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-    const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
-    const T* J = cr + CR_J + r * CJ;
-    const T* Jb = J + nda;
-    O s = 0;
+  constexpr int U = jx_rounds<DIM>();
+  const int ne = 3 * ncon;
+  for (int e0 = LANE; e0 < ne; e0 += U * WAVE) {
+    O s[U];
 #pragma unroll
-    for (int j = 0; j < 9; j++) {
-      const T ja = J[j];
-      const X xa = x[oa + j];
-      s += (j < nda ? (O)ja : O(0)) * (O)xa;
+    for (int u = 0; u < U; u++) {
+      const int e = e0 + u * WAVE < ne ? e0 + u * WAVE : 0;
+      const int c = e / 3, r = e - 3 * c;
+      const int* ci = w.ci() + 4 * c;
+      const T* cr = w.cr() + CR_N * c;
+      const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+      const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+      const T* J = cr + CR_J + r * CJ;
+      const T* Jb = J + nda;
+      O acc = 0;
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        const T ja = J[j];
+        const X xa = x[oa + j];
+        acc += (j < nda ? (O)ja : O(0)) * (O)xa;
+      }
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        const T jb = Jb[j];
+        const X xb = x[ob + j];
+        acc += (j < ndb ? (O)jb : O(0)) * (O)xb;
+      }
+      s[u] = acc;
     }
 #pragma unroll
-    for (int j = 0; j < 9; j++) {
-      const T jb = Jb[j];
-      const X xb = x[ob + j];
-      s += (j < ndb ? (O)jb : O(0)) * (O)xb;
+    for (int u = 0; u < U; u++) {
+      const int e = e0 + u * WAVE;
+      if (e < ne) {
+        const int c = e / 3, r = e - 3 * c;
+        ((O*)(w.cr() + CR_N * c + slot))[r] = s[u];
+      }
     }
-    ((O*)(cr + slot))[r] = s;
   }
 }
 
@@ -3995,29 +4033,46 @@ template <typename T, typename DIM>
 __device__ __forceinline__ void rows_eval2(const Model<T>& M, const Ws<T, DIM>& w, const T* xs, const double* xw,
                                            int ncon, int nrow) {
   const DIM dm(M.dm);
-  for (int e = LANE; e < 3 * ncon; e += WAVE) {
-    const int c = e / 3, r = e - 3 * c;
-    const int* ci = w.ci() + 4 * c;
-    T* cr = w.cr() + CR_N * c;
-    const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-    const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
-    const T* J = cr + CR_J + r * CJ;
-    const T* Jb = J + nda;
-    double s1 = 0, s2 = 0;
+  constexpr int U = jx_rounds<DIM>();
+  const int ne = 3 * ncon;
+  for (int e0 = LANE; e0 < ne; e0 += U * WAVE) {
+    double s1[U], s2[U];
 #pragma unroll
-    for (int j = 0; j < 9; j++) {
-      const double ja = j < nda ? (double)J[j] : 0.0;
-      s1 += ja * (double)xs[oa + j];
-      s2 += ja * xw[oa + j];
+    for (int u = 0; u < U; u++) {
+      const int e = e0 + u * WAVE < ne ? e0 + u * WAVE : 0;  // past the last item: record 0, result unused
+      const int c = e / 3, r = e - 3 * c;
+      const int* ci = w.ci() + 4 * c;
+      const T* cr = w.cr() + CR_N * c;
+      const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
+      const int oa = ta >= 0 ? tree_dof(dm, ta) : 0, ob = tb >= 0 ? tree_dof(dm, tb) : 0;
+      const T* J = cr + CR_J + r * CJ;
+      const T* Jb = J + nda;
+      double a1 = 0, a2 = 0;
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        const double ja = j < nda ? (double)J[j] : 0.0;
+        a1 += ja * (double)xs[oa + j];
+        a2 += ja * xw[oa + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        const double jb = j < ndb ? (double)Jb[j] : 0.0;
+        a1 += jb * (double)xs[ob + j];
+        a2 += jb * xw[ob + j];
+      }
+      s1[u] = a1;
+      s2[u] = a2;
     }
 #pragma unroll
-    for (int j = 0; j < 9; j++) {
-      const double jb = j < ndb ? (double)Jb[j] : 0.0;
-      s1 += jb * (double)xs[ob + j];
-      s2 += jb * xw[ob + j];
+    for (int u = 0; u < U; u++) {
+      const int e = e0 + u * WAVE;
+      if (e < ne) {
+        const int c = e / 3, r = e - 3 * c;
+        T* cr = w.cr() + CR_N * c;
+        dslot(cr, CR_JD)[r] = s1[u];
+        dslot(cr, CR_JA)[r] = s2[u];
+      }
     }
-    dslot(cr, CR_JD)[r] = s1;
-    dslot(cr, CR_JA)[r] = s2;
   }
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
@@ -4440,8 +4495,8 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
   }
   const float S = wave_sum(s_t), LY = wave_sum(ly_t);
   // ---- the coupled system + belt (position m), in LDS with row stride n
-  double* const grest = w.tmp();                  // right-hand side (chol_solve_reg negates it)
-  float* const xr = (float*)(w.tmp() + TB_MAXR);  // its solution
+  double* const grest = (double*)(tbw + tb_rhs(NT));  // right-hand side (chol_solve_reg negates it)
+  float* const xr = tbw + tb_sol(NT);                  // its solution
   for (int e = LANE; e < n * n; e += WAVE) {
     const int i = e / n, j = e - n * (e / n);
     if (i < m && j < m) {
@@ -5357,10 +5412,22 @@ __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w
 // maps / last_ctrl / move_start updated in the arena's IK block.  Reads the float64 master state; uses the
 // phase-local H region as scratch (free outside a substep's stage / solve).  Not inlined (it runs a few times
 // per env-step): every pointer it receives is global or LDS -- none into a caller's private frame, which a
-// callee could only reach through the flat scratch aperture.
-__device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const double* ctrlrange_d, IkTiming tm, int A, int K,
-                                            const double* qd, const double* vd, int32_t* ti, double* td,
-                                            int int_base, int dbl_base, double* scr, double* prop) {
+// callee could only reach through the flat scratch aperture.  Every pointer parameter carries its address space
+// (scene tables constant, master state LDS, task records global, scratch SAS = LDS or the arena's global block):
+// through a generic parameter each access would be a FLAT instruction.
+template <int SAS>
+__device__ __noinline__ void ik_compose_raw(const double FM_AS(4)* arm_base_g, const double FM_AS(4)* ctrlrange_g,
+                                            IkTiming tm, int A, int K, const double FM_AS(3)* qd_, const double FM_AS(3)* vd_,
+                                            int32_t FM_AS(1)* ti_, double FM_AS(1)* td_, int int_base, int dbl_base,
+                                            double FM_AS(SAS)* scr_, double FM_AS(SAS)* prop_) {
+  const double* arm_base_w = (const double*)arm_base_g;
+  const double* ctrlrange_d = (const double*)ctrlrange_g;
+  const double* qd = (const double*)qd_;
+  const double* vd = (const double*)vd_;
+  int32_t* ti = (int32_t*)ti_;
+  double* td = (double*)td_;
+  double* scr = (double*)scr_;
+  double* prop = (double*)prop_;
   // scr per arm (24): grip 3 | tpos 3 | tquat 4 | need | close | pad 2 | q 7 | pad 3
   struct D {
     int A, K;
@@ -5400,7 +5467,7 @@ __device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const doub
     if (sc[10] != 0.0) {
       double* q = sc + 14;  // the arm's private copy of its hinges (qpos_from_site_pose, inplace=False), in LDS
       for (int j = 0; j < 7; j++) q[j] = qd[1 + 7 * K + 9 * LANE + j];
-      ok = ik_solve(arm_base_w + 12 * LANE, q, sc + 3, sc + 6) != 0;
+      ok = ik_solve<SAS>(arm_base_g + 12 * LANE, scr_ + 24 * LANE + 14, scr_ + 24 * LANE + 3, scr_ + 24 * LANE + 6) != 0;
       if (ok) {
         for (int j = 0; j < 7; j++) ctrl[j] = q[j];
         ctrl[7] = sc[11] != 0.0 ? 0.0 : 2.0;
@@ -5420,7 +5487,11 @@ __device__ __noinline__ void ik_compose_raw(const double* arm_base_w, const doub
 template <typename T, typename DIM>
 __device__ __forceinline__ void ik_compose(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td, double* prop) {
   const DIM dm(M.dm);
-  ik_compose_raw(M.arm_base_w, M.ctrlrange_d, M.ik_time, dm.A, dm.K, w.qd(), w.vd(), ti, td, 0, 0, (double*)w.H(), prop);
+  constexpr int SAS = DIM::spill ? AS_GLOBAL : AS_LDS;  // where w.H() (the compose scratch) lives
+  ik_compose_raw<SAS>((const double FM_AS(4)*)(const double*)M.arm_base_w,
+                      (const double FM_AS(4)*)(const double*)M.ctrlrange_d, M.ik_time, dm.A, dm.K,
+                      (const double FM_AS(3)*)w.qd(), (const double FM_AS(3)*)w.vd(), (int32_t FM_AS(1)*)ti,
+                      (double FM_AS(1)*)td, 0, 0, (double FM_AS(SAS)*)w.H(), (double FM_AS(SAS)*)prop);
 }
 
 // IKTogglingEnv._process_observation (environments.py:560-577): fresh proposals, kept for the next step's
@@ -5654,9 +5725,12 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
           p.pause_last()[j] = c;  // last_arm_actions = arm_actions (environments.py:608-611)
           break;
         }
-        case FM_ENV_BACKUP_IK_TOGGLE:
-          c = act[arm] == 1.0f ? ik_arm(dm, ti, td, arm).ik_actions()[j] : IK_DEFAULT_POSE[j];
+        case FM_ENV_BACKUP_IK_TOGGLE: {
+          // values selected, not pointers (a select of the global record and the constant table is a FLAT load)
+          const double ia = ik_arm(dm, ti, td, arm).ik_actions()[j], dp = IK_DEFAULT_POSE[j];
+          c = act[arm] == 1.0f ? ia : dp;
           break;
+        }
         default:  // FM_ENV_FACTORY
           c = prop[u - 1];
       }

@@ -209,8 +209,16 @@ __device__ __forceinline__ void chol_solve_d(double* A, double* x) {
   }
 }
 
-// qpos_from_site_pose on the arm's 7 hinges (oracle or_ik_solve); q is updated in place, returns success
-__device__ __noinline__ int ik_solve(const double* base, double* q, const double* tpos, const double* tquat) {
+// qpos_from_site_pose on the arm's 7 hinges (oracle or_ik_solve); q is updated in place, returns success.
+// Not inlined: base is the scene table (constant address space), q / tpos / tquat the compose scratch (address
+// space SAS: LDS, or the arena's global block in the spill layouts) -- no generic pointer, no FLAT access
+template <int SAS>
+__device__ __noinline__ int ik_solve(const double FM_AS(4)* base_, double FM_AS(SAS)* q_, const double FM_AS(SAS)* tpos_,
+                                     const double FM_AS(SAS)* tquat_) {
+  const double* base = (const double*)base_;
+  double* q = (double*)q_;
+  const double* tpos = (const double*)tpos_;
+  const double* tquat = (const double*)tquat_;
   int success = 0;
   for (int steps = 0; steps < 10; steps++) {
     double sp[3], sR[9], anc[7][3], ax[7][3];

@@ -484,6 +484,19 @@ class FactoryVecEnv:
         _lib.check(self._L.fm_get_costs(self._h, out.ctypes.data_as(C.c_void_p)))
         return out
 
+    def kernel_timing(self, enable=True):
+        """time each env-step kernel launch alone (fm_kernel_timing: a HIP event pair on the env's stream around the
+        step kernel; the dispatch-order kernel and the wide rerun launch stay outside)"""
+        self._bind_stream()
+        _lib.check(self._L.fm_kernel_timing(self._h, 1 if enable else 0))
+
+    def kernel_time(self):
+        """(summed milliseconds, launches) of the step-kernel launches since the last call (fm_get_kernel_time)"""
+        self._bind_stream()
+        ms, n = C.c_double(0.0), C.c_int(0)
+        _lib.check(self._L.fm_get_kernel_time(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     PHASES = ["fk", "geoms_mass", "collision", "rows", "smooth_acc", "newton_setup", "newton_grad",
               "newton_hessian", "newton_chol", "newton_solve", "newton_linesearch", "newton_final",
               "integrate", "task_obs", None, None, "coll_bounds", "coll_midphase", "coll_narrow",

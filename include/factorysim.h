@@ -158,6 +158,13 @@ int fm_num_counters(void);
 /* Diagnostic: each arena's last env-step duration in GPU wall-clock ticks (host [N] uint32; 0 until its first step;
  * the longest-first dispatch order of the next step is sorted by these) -- the launch's load balance. */
 int fm_get_costs(fm_handle* h, uint32_t* host_out);
+/* Measurement: time each env-step kernel launch alone with a HIP event pair on the handle's stream (enable != 0;
+ * enabling or disabling discards earlier records).  fm_get_kernel_time synchronises the stream and returns the
+ * summed duration of the step-kernel launches recorded since the last read (the longest-first order kernel, the
+ * rerun-list reset and the (2,4) wide rerun launch are outside the pairs), then starts a new record.  bench.py's
+ * roofline.achieved divides the algorithmic bytes by this per-launch time. */
+int fm_kernel_timing(fm_handle* h, int enable);
+int fm_get_kernel_time(fm_handle* h, double* total_ms, int* launches);
 
 /* Diagnostic: wall-clock phase profile of fm_step summed over arenas (host [24] uint64).
  * mode 1 = zero and enable, 0 = disable, -1 = leave as is; host_out (may be NULL) receives the

@@ -115,14 +115,19 @@ def entry_name(A, K, j, dbl):
     return f"{'qpos' if isq else 'qvel'}[{i}] ({body})"
 
 
-def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv", verbose_tol=None, **kw):
+def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv", verbose_tol=None, alt=None, **kw):
     """one teacher-forced env-step per trajectory step, all in one launch.  Returns per-step relative state
-    errors, the steps whose integer task state / flags disagree, obs and reward errors, the counters"""
+    errors, the steps whose integer task state / flags disagree, obs and reward errors, the counters.
+
+    alt: the same states and actions stepped by a second oracle (restep_at_tolerance at MuJoCo's 1e-8): then
+    errs_min[i] = min(error against the trajectory's oracle, error against alt) on the same compared steps -- at a
+    bifurcation the two oracles themselves part, and the kernel is right if it follows either"""
     import torch
 
     from factory_marl_amd import state as st
 
     recs, acts, outs = trajectory
+    alt_outs = alt[2] if alt is not None else None
     n = len(recs)
     experiment = kw.pop("experiment", "")
     env = gpu_env(n, precision, A, K, env_class, **kw)
@@ -135,7 +140,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     obs, rew, term = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
     tobs = env.terminal_obs.cpu().numpy()
     nq = 1 + 7 * K + 9 * A
-    errs, err_steps, int_bad, flag_bad, obs_err, rew_err, ik_err = [], [], [], [], [], [], []
+    errs, err_steps, int_bad, flag_bad, obs_err, rew_err, ik_err, errs_min = [], [], [], [], [], [], [], []
     reset_bad, reset_err = [], []
     for s in range(n):
         o = outs[s]
@@ -163,6 +168,13 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
         qd, vd = state_err(A, K, gd, o["dbl"])
         errs.append(max(qd.max(), vd.max()))
         err_steps.append(s)
+        if alt_outs is not None:
+            ao = alt_outs[s]
+            if ao["term"]:
+                errs_min.append(errs[-1])
+            else:
+                qa, va = state_err(A, K, gd, ao["dbl"])
+                errs_min.append(min(errs[-1], max(qa.max(), va.max())))
         if verbose_tol is not None and errs[-1] > verbose_tol:
             j = int(np.argmax(np.concatenate([qd, vd])))
             print(f"  step {s}: worst {entry_name(A, K, j, o['dbl'])} "
@@ -172,6 +184,7 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     cnt = env.counters()
     env.close()
     return dict(errs=np.array(errs), err_steps=np.array(err_steps, int), int_bad=int_bad, flag_bad=flag_bad,
+                errs_min=np.array(errs_min) if alt_outs is not None else None,
                 reset_bad=reset_bad, reset_err=np.array(reset_err), resets=len(reset_err),
                 obs_err=np.array(obs_err), rew_err=np.array(rew_err), counters=cnt, ik_err=np.array(ik_err),
                 terms=int(sum(o["term"] for o in outs)), max_cubes=max(o["info"]["num_obj"] for o in outs))
@@ -189,3 +202,15 @@ def summary(r, gate=1e-4):
                 missing_steps=[int(s) for s in r["err_steps"][e > gate]],
                 resets_compared=r.get("resets", 0), reset_bad=len(r.get("reset_bad", [])),
                 reset_worst=float(r["reset_err"].max()) if r.get("resets", 0) else 0.0)
+
+
+def two_oracle_gate(r, frac=0.99, cap=1e-3, gate=1e-4):
+    """the per-step gate against the two oracles (compare(..., alt=...)): min(error vs the 1e-12 oracle, error vs
+    the 1e-8 oracle) within the SURVEY gate on >= frac of the compared steps and <= cap on every step.  Returns
+    (fraction within, worst, missing steps)"""
+    e = r["errs_min"]
+    within = float(np.mean(e <= gate)) if len(e) else 1.0
+    worst = float(e.max()) if len(e) else 0.0
+    missing = [int(x) for x in r["err_steps"][e > gate]]
+    assert within >= frac and worst <= cap, (within, worst, missing)
+    return within, worst, missing

@@ -44,3 +44,47 @@ def test_sync_is_a_wave_barrier_with_fences():
     body = m.group(1)
     assert "__builtin_amdgcn_wave_barrier" in body
     assert "__ATOMIC_RELEASE" in body and "__ATOMIC_ACQUIRE" in body and '"wavefront"' in body
+
+
+def _isa():
+    import importlib.util
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    so = root / "factory_marl_amd" / "libfactorysim.so"
+    if not so.exists() or not pathlib.Path("/opt/rocm/lib/llvm/bin/llvm-objdump").exists():
+        import pytest
+
+        pytest.skip("libfactorysim.so not built (python -c 'import __graft_entry__ as g; g.build()') or no ROCm llvm")
+    spec = importlib.util.spec_from_file_location("isa_flat", root / "tools" / "isa_flat.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.scan(str(so))
+
+
+_SCAN = {}
+
+
+def _scan():
+    if "r" not in _SCAN:
+        _SCAN["r"] = _isa()
+    return _SCAN["r"]
+
+
+def test_no_flat_instructions_in_the_library():
+    """every device function of libfactorysim.so (step / reset / debug kernels and the non-inlined IK functions)
+    accesses memory through address-space-specific instructions: no flat_load / flat_store / flat_atomic.  A FLAT
+    access is a pointer whose address space the compiler lost (a pointer selected between LDS and global or
+    kernarg memory, a generic parameter of a non-inlined function); round 4's aperture-violation fault came from the
+    one kernel family that carried them"""
+    flat, _ = _scan()
+    bad = {f"{co}: {fn[:90]}": dict(c) for (co, fn), c in flat.items()}
+    assert not bad, bad
+
+
+def test_step_kernels_have_a_fixed_private_segment():
+    """no step kernel needs a dynamic stack (the private segment the runtime allocates is the one the code object
+    declares)"""
+    _, meta = _scan()
+    ks = {k: v for k, v in meta.items() if "step_kernel" in k[1]}
+    assert ks
+    assert not [k for k, v in ks.items() if v.get("uses_dynamic_stack")], ks

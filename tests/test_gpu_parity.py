@@ -77,10 +77,17 @@ def long_trajectory(oracle):
     return _rollout(oracle, A, K, 300, seed_actions=21)
 
 
+@pytest.fixture(scope="module")
+def long_trajectory_tol8(oracle, long_trajectory):
+    """the long trajectory's states and actions stepped by the oracle at MuJoCo's 1e-8 Newton tolerance"""
+    return pu.restep_at_tolerance(oracle, A, K, long_trajectory, 1e-8)
+
+
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 @pytest.mark.parametrize("which", ["short", "long"])
-def test_teacher_forced_fp32(trajectory, long_trajectory, which):
-    r = _compare(trajectory if which == "short" else long_trajectory, "fp32", 1e-4)
+def test_teacher_forced_fp32(trajectory, long_trajectory, long_trajectory_tol8, which):
+    r = pu.compare(trajectory if which == "short" else long_trajectory, "fp32", A, K, verbose_tol=1e-3,
+                   alt=None if which == "short" else long_trajectory_tol8)
     e = r["errs"]
     frac = float(np.mean(e <= 1e-4))
     print(f"fp32 teacher-forced (SURVEY tolerance 1e-4 rel): {frac:.1%} of {len(e)} steps within; "
@@ -98,8 +105,12 @@ def test_teacher_forced_fp32(trajectory, long_trajectory, which):
     else:
         # round 4 (contact points relative to their cube, profiles/r04_parity.md): 296 of 299 steps -- the first
         # landing (step 6, 3.4e-4), a cube spinning at 3.8 rad/s (step 112, 1.05e-4) and step 166 (0.133, a struck
-        # spinning cube, missed the same way by the float64 oracle at MuJoCo's 1e-8 tolerance)
-        assert frac >= 0.989 and np.sort(e)[-2] <= 1e-3 and e.max() <= 0.15, (frac, np.sort(e)[-3:])
+        # spinning cube, missed the same way by the float64 oracle at MuJoCo's 1e-8 tolerance).  Step 166 is a
+        # bifurcation on which the 1e-12 and the 1e-8 oracle part: the per-step gate takes the nearer of the two --
+        # within 1e-4 on >= 99 % of the steps and <= 1e-3 on every step (no cap of 0.15 on any step)
+        assert frac >= 0.989, (frac, np.sort(e)[-3:])
+        within, worst, missing = pu.two_oracle_gate(r, frac=0.99, cap=1e-3)
+        print(f"  nearer of the 1e-12 / 1e-8 oracles: {within:.2%} within 1e-4, worst {worst:.2e}, missing {missing}")
     assert np.median(e) <= 1e-5
     # the same algorithm in plain single precision (liboracle_f32.so, tools/fp32_floor.py --float-oracle) on the
     # same trajectory: the kernel (float64 master state, z-shifted frame) must hold the gate at least as often,
@@ -296,35 +307,26 @@ def test_masked_reset_only_touches_masked_arenas():
     env.close()
 
 
-# (4,16) fp32 gates per env class and oracle: (fraction within 1e-4, cap on the second-worst step, cap on the worst)
-# -- round 4 (profiles/r04_parity.md): Backup 99.3 % / 100 % within against the 1e-12 / 1e-8 oracles, worst 5.5e-4 /
-# 3.9e-5; Pause 98.6 % against both, misses step 23 (4.5e-4) and step 142 -- a bifurcation where the 1e-12 and the
-# 1e-8 oracle themselves differ by 0.92 relative, and the kernel's branch follows one or the other with the last bits
-# of its arithmetic (it followed the 1e-8 oracle at r04d, the 1e-12 one at r04f)
-CONFIG5_GATES = {"PauseIKToggleEnv": {"1e-12": (0.98, 1e-3, 1.0), "1e-8": (0.98, 1e-3, 1.0)},
-                 "BackupIKToggleEnv": {"1e-12": (0.99, 1e-3, 1e-3), "1e-8": (0.99, 1e-3, 1e-3)}}
-
-
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-@pytest.mark.parametrize("env_class", sorted(CONFIG5_GATES))
+@pytest.mark.parametrize("env_class", ["BackupIKToggleEnv", "PauseIKToggleEnv"])
 def test_config5_scene_4x16_fp32(oracle, env_class):
     """BASELINE config 5's arena (4 arms x 16 cubes, the toggle env classes, environments.py:580-645) in the
     benchmarked compile-time fp32 kernel, teacher-forced over 150 env-steps from reset against the float64 oracle and
-    against the oracle restepped at MuJoCo's 1e-8 Newton tolerance: no contact dropped (the scene exceeds 64), IK / task
-    integer state exact, the SURVEY gate on the measured fraction with the worst step capped"""
+    the oracle restepped at MuJoCo's 1e-8 Newton tolerance (one GPU launch): no contact dropped (the scene exceeds
+    64), IK / task integer state exact, and per step the nearer of the two oracles within the SURVEY gate on >= 99 %
+    of the steps and within 1e-3 on every step.  (Round 4: the Pause toggle's step 142 is a bifurcation where the
+    1e-12 and the 1e-8 oracle differ by 0.92 relative; the kernel follows one of them, profiles/r04_parity.md)"""
     traj = pu.rollout(oracle, 4, 16, 150, seed_actions=3, env_class=env_class)
     tol8 = pu.restep_at_tolerance(oracle, 4, 16, traj, 1e-8, env_class)
-    for name, t in [("1e-12", traj), ("1e-8", tol8)]:
-        gate, cap2, cap = CONFIG5_GATES[env_class][name]
-        r = pu.compare(t, "fp32", 4, 16, env_class)
-        e = r["errs"]
-        frac = float(np.mean(e <= 1e-4))
-        print(f"fp32 (4,16) {env_class} vs the {name} oracle: {frac:.1%} within 1e-4, median {np.median(e):.2e}, "
-              f"worst {e.max():.2e}, missing {list(r['err_steps'][e > 1e-4])}, max contacts "
-              f"{int(r['counters'][:, 5].max())}, dropped {int(r['counters'][:, 0].sum())}")
-        assert r["counters"][:, 0].sum() == 0 and r["counters"][:, 5].max() > 64
-        assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"])
-        assert frac >= gate and np.sort(e)[-2] <= cap2 and e.max() <= cap, (frac, np.sort(e)[-3:])
+    r = pu.compare(traj, "fp32", 4, 16, env_class, alt=tol8)
+    e = r["errs"]
+    print(f"fp32 (4,16) {env_class} vs the 1e-12 oracle: {np.mean(e <= 1e-4):.1%} within 1e-4, median "
+          f"{np.median(e):.2e}, worst {e.max():.2e}, missing {list(r['err_steps'][e > 1e-4])}, max contacts "
+          f"{int(r['counters'][:, 5].max())}, dropped {int(r['counters'][:, 0].sum())}")
+    assert r["counters"][:, 0].sum() == 0 and r["counters"][:, 5].max() > 64
+    assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"])
+    within, worst, missing = pu.two_oracle_gate(r, frac=0.99, cap=1e-3)
+    print(f"  nearer of the two oracles: {within:.1%} within 1e-4, worst {worst:.2e}, missing {missing}")
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
@@ -431,22 +433,127 @@ def _crowded_states(oracle, n_states, lo=66, hi=110, seed=0):
     return np.stack(recs)
 
 
-@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-def test_contacts_above_64_are_not_dropped(oracle):
-    """(2,4) benchmark scene, env-steps whose stages hold more than 64 contacts (both arms reaching into the table, the
-    belt and each other; the parked cubes' 16 floor contacts): the 64-contact launch abandons them and the wide
-    kernel steps them -- no contact is dropped, and from the same records the oracle (which keeps every contact,
-    base_env.py:217-218 -> mj_step) gives the same result: fp64 within 1e-7, integer state / flags exact"""
+def _calm_crowded_states(oracle, n_states, seed=1):
+    """(2,4) records whose first stage holds 66-100 contacts without a force termination: the arms moved from the
+    parked pose towards a random pose that reaches into the table / belt / each other only as far as the contact
+    count needs (bisection on the path to a target count), at rest, with the control target and the actions holding
+    that pose -- so the env-step is compared as a state, not only through its terminal observation.  Kept when the
+    oracle's env-step from it does not terminate.  Returns (records, actions)"""
+    from factory_marl_amd import state as st
+
+    e = oracle.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4))
+    e.reset()
+    for _ in range(8):
+        e.step(np.zeros(8 * A, np.float32))
+    d0, i0, r0 = e.export_state()
+    nq, nv = st.sizes(A, K)[:2]
+    a0 = 1 + 7 * K
+    lim = np.asarray(e.model.ctrlrange).reshape(-1, 2)
+    off = 2 * nq + 3 * nv  # ctrl_target in the float64 record
+    base = d0[:nq].copy()
+    rng = np.random.default_rng(seed)
+
+    def ncon(q):
+        e.data.qpos[:] = q
+        e.data.forward()
+        return e.data.ncon
+
+    recs, acts = [], []
+    for _ in range(20000):
+        q = base.copy()
+        for arm in range(A):
+            b = a0 + 9 * arm
+            q[b:b + 7] = [rng.uniform(-1, 1), rng.uniform(-2.09, 2.09), rng.uniform(-1, 1), rng.uniform(-2.09, 2.09),
+                          rng.uniform(-1, 1), rng.uniform(-2.09, 2.09), 0.0]
+        target = int(rng.integers(66, 90))
+        if ncon(q) < target:
+            continue
+        lo_t, hi_t = 0.0, 1.0
+        for _ in range(12):
+            m = 0.5 * (lo_t + hi_t)
+            lo_t, hi_t = (lo_t, m) if ncon(base + m * (q - base)) >= target else (m, hi_t)
+        qc = base + hi_t * (q - base)
+        if not 66 <= ncon(qc) <= 100:
+            continue
+        d = d0.copy()
+        d[:nq] = qc
+        d[nq + nv:2 * nq + nv] = qc
+        d[nq:nq + nv] = 0.0
+        d[2 * nq + nv:2 * nq + 2 * nv] = 0.0
+        a = np.zeros(8 * A, np.float32)
+        for arm in range(A):
+            for j in range(8):
+                lo_, hi_ = lim[1 + 8 * arm + j]
+                qq = qc[a0 + 9 * arm + j] if j < 7 else d[off + 1 + 8 * arm + j]
+                d[off + 1 + 8 * arm + j] = qq
+                a[8 * arm + j] = np.arctanh(np.clip(2 * (qq - lo_) / (hi_ - lo_) - 1, -0.999999, 0.999999))
+        rec = st.pack(A, K, d, i0, r0)
+        e.import_state(*st.unpack(A, K, rec))
+        if e.step(a)[2]:
+            continue  # force termination: not a calm state
+        recs.append(rec)
+        acts.append(a)
+        if len(recs) == n_states:
+            break
+    return np.stack(recs), np.stack(acts)
+
+
+def _crowded_trajectory(oracle):
+    """12 crowded records (arms deep in the table: most force-terminate) + 10 calm ones (compared as states)"""
     recs = _crowded_states(oracle, 12)
     acts = np.random.default_rng(4).uniform(-1, 1, (len(recs), 8 * A)).astype(np.float32)
-    traj = pu.restep_at_tolerance(oracle, A, K, (recs, acts, None), 0.0)
-    r = pu.compare(traj, "fp64", A, K)
+    crec, cact = _calm_crowded_states(oracle, 10)
+    recs, acts = np.concatenate([recs, crec]), np.concatenate([acts, cact])
+    return pu.restep_at_tolerance(oracle, A, K, (recs, acts, None), 0.0)
+
+
+@pytest.fixture(scope="module")
+def crowded(oracle):
+    traj = _crowded_trajectory(oracle)
+    return traj, pu.restep_at_tolerance(oracle, A, K, traj, 1e-8)
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_contacts_above_64_are_not_dropped(crowded, precision):
+    """(2,4) benchmark scene, env-steps whose stages hold more than 64 contacts (arms reaching into the table, the belt
+    and each other; the parked cubes' 16 floor contacts): the 64-contact launch abandons them and the wide kernel
+    steps them -- no contact is dropped, and from the same records the oracle (which keeps every contact,
+    base_env.py:217-218 -> mj_step) gives the same result.  >= 8 of the records do not terminate, so they are
+    compared as states: fp64 within 1e-7; fp32 (the wide kernel of the benchmarked build) at the SURVEY gate against
+    the nearer of the 1e-12 / 1e-8 oracles; integer state / flags exact in both"""
+    traj, tol8 = crowded
+    recs = traj[0]
+    r = pu.compare(traj, precision, A, K, alt=tol8 if precision == "fp32" else None, verbose_tol=1e-4)
     e = r["errs"]
-    print(f">64-contact env-steps: {len(recs)}, compared {len(e)} (+{r['terms']} terminations), worst "
+    print(f"{precision} >64-contact env-steps: {len(recs)}, compared {len(e)} (+{r['terms']} terminations), worst "
           f"{e.max() if len(e) else 0:.2e}, reruns {int(r['counters'][:, 8].sum())}, max contacts "
           f"{int(r['counters'][:, 5].max())}, dropped {int(r['counters'][:, 0].sum())}")
-    assert len(recs) == 12 and int(r["counters"][:, 5].max()) > 64 and int(r["counters"][:, 0].sum()) == 0
+    assert len(recs) == 22 and int(r["counters"][:, 5].max()) > 64 and int(r["counters"][:, 0].sum()) == 0
     assert int(r["counters"][:, 8].sum()) == len(recs)  # each one went through the wide kernel
     assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"], r["reset_bad"])
-    assert (e.max() if len(e) else 0.0) <= 1e-7
-    assert r["obs_err"].max() <= 1e-5
+    assert len(e) >= 8  # compared as states, not only through their terminal observations
+    if precision == "fp64":
+        assert e.max() <= 1e-7
+        assert r["obs_err"].max() <= 1e-5
+    else:
+        within, worst, missing = pu.two_oracle_gate(r, frac=0.9, cap=1e-3)
+        print(f"  nearer of the two oracles: {within:.1%} within 1e-4, worst {worst:.2e}, missing {missing}")
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("env_class", ["PauseIKToggleEnv", "AllDeltaProgressRewardEnv"])
+def test_wide_rerun_kernel_ik_classes_fp64(oracle, env_class):
+    """the rerun path of the IK classes (FM_FORCE_RERUN=1: every (2,4) env-step abandoned by the 64-contact kernel
+    after its IK compose wrote the FSM / toggle blocks, then restored from State::bak and stepped by the wide kernel)
+    against the oracle in fp64 with the gates of the 64-contact kernel's IK-class test: IK FSM block and every integer
+    exact, IK doubles within 1e-6, state within 1e-5 (grasps put the stiff gripper contacts on a cube)"""
+    traj = pu.rollout(oracle, A, K, 120, seed_actions=13, env_class=env_class)
+    r = pu.compare(traj, "fp64", A, K, env_class, experiment="FM_FORCE_RERUN=1")
+    e = r["errs"]
+    print(f"fp64 wide rerun {env_class}: worst {e.max():.2e}, IK block {r['ik_err'].max():.2e}, reruns "
+          f"{int(r['counters'][:, 8].sum())}, terms {r['terms']}")
+    assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"], r["reset_bad"])
+    assert int(r["counters"][:, 8].sum()) == len(traj[0])
+    assert e.max() <= 1e-5 and r["ik_err"].max() <= 1e-6
+    assert r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6

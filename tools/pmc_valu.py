@@ -5,7 +5,8 @@ usage: python tools/pmc_valu.py PMC.csv --arenas 4096 --last 3 [--precision fp32
 Counters (one pass, 8 SQ slots): SQ_INSTS_VALU, SQ_INSTS_VALU_ADD_F32, SQ_INSTS_VALU_MUL_F32, SQ_INSTS_VALU_FMA_F32,
 SQ_INSTS_VALU_TRANS_F32, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAVES.  Instruction counters count wave-instructions:
 lane FLOPs = 64 x (ADD + MUL + TRANS + 2 FMA) -- every lane of the wave, active or not, so an upper bound on the
-useful fp32 FLOPs.  Only the last `--last` step_kernel dispatches are used (the timed steps after the pre-roll).
+useful fp32 FLOPs.  Only the last `--last` dispatches of the step-kernel instantiation with the most waves are used (the timed steps after
+the pre-roll; SQ_WAVES = the arena count per launch).
 """
 import argparse
 import csv
@@ -23,13 +24,22 @@ def main():
     ap.add_argument("--objects", type=int, default=4)
     ap.add_argument("--out", default="profiles/pmc_valu.json")
     a = ap.parse_args()
+    # per dispatch, per step-kernel instantiation: the (2,4) bench launches the wide rerun kernel after every step
+    # (nearly always over an empty list, a few waves) -- only the instantiation with the most waves per dispatch is
+    # the step kernel the line prices (as tools/pmc_traffic.py selects it)
     per = defaultdict(dict)
+    kname = {}
     for r in csv.DictReader(open(a.csv)):
         if "step_kernel" not in r["Kernel_Name"]:
             continue
         key = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+        kname[key] = r["Kernel_Name"]
         per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    keys = sorted(per)[-a.last:]
+    waves = defaultdict(list)
+    for k, c in per.items():
+        waves[kname[k]].append(c.get("SQ_WAVES", 0.0))
+    main_k = max(waves, key=lambda n: sorted(waves[n])[len(waves[n]) // 2])
+    keys = sorted(k for k in per if kname[k] == main_k)[-a.last:]
     tot = defaultdict(float)
     for k in keys:
         for c, v in per[k].items():
@@ -38,7 +48,7 @@ def main():
     f = "F32" if a.precision == "fp32" else "F64"
     flop = 64.0 * (tot.get(f"SQ_INSTS_VALU_ADD_{f}", 0) + tot.get(f"SQ_INSTS_VALU_MUL_{f}", 0) +
                    tot.get(f"SQ_INSTS_VALU_TRANS_{f}", 0) + 2 * tot.get(f"SQ_INSTS_VALU_FMA_{f}", 0))
-    rec = {"kernel": "fm::step_kernel", "arenas": n, "precision": a.precision, "A": a.arms, "K": a.objects,
+    rec = {"kernel": main_k, "arenas": n, "precision": a.precision, "A": a.arms, "K": a.objects,
            "dispatches": len(keys), "counters_per_launch": dict(tot),
            "valu_wave_instr_per_arena_step": tot.get("SQ_INSTS_VALU", 0) / n,
            "valu_lane_flops_per_arena_step": flop / n,
