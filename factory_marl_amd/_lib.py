@@ -42,6 +42,7 @@ class FmConfig(C.Structure):
         ("base_reward", C.c_double),
         ("solver_iterations", C.c_int32),
         ("solver_tolerance", C.c_double),
+        ("obs_float64", C.c_int32),
     ]
 
 

@@ -200,6 +200,7 @@ static Model<T> make_model(const fm_handle* h) {
   M.prof = h->prof_on ? h->prof : nullptr;
   M.dbg_flags = h->xflags;
   M.ovf_abort = 0;
+  M.obs64 = c.obs_float64 != 0;
   return M;
 }
 
@@ -922,8 +923,9 @@ int fm_nv(const fm_handle* h) { return h ? h->dm.nv : -1; }
 int fm_nu(const fm_handle* h) { return h ? h->dm.nu : -1; }
 int fm_workspace_bytes(const fm_handle* h) { return h ? h->lay_step.total : -1; }
 
-int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
+int fm_reset(fm_handle* h, const uint8_t* mask, void* obs_) {
   if (!h) return set_err(FM_EINVAL, "null handle");
+  float* obs = (float*)obs_;  // float64 rows when cfg.obs_float64 (Model::obs64): the kernel writes the row type
   HIPCHK(hipSetDevice(h->device));
   dim3 grid(h->dm.N), block(WAVE);
   if (h->fp64 && h->spill) {
@@ -941,7 +943,7 @@ int fm_reset(fm_handle* h, const uint8_t* mask, float* obs) {
   return FM_OK;
 }
 
-int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+int fm_step(fm_handle* h, const float* actions, void* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
             const fm_info* info) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   if (!actions && h->dm.act_dim > 0) return set_err(FM_EINVAL, "actions is NULL");
@@ -950,7 +952,7 @@ int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8
   StepIO io;
   std::memset(&io, 0, sizeof io);
   io.actions = actions;
-  io.obs = obs;
+  io.obs = (float*)obs;  // float64 rows when cfg.obs_float64 (Model::obs64)
   io.reward = reward;
   io.terminated = terminated;
   io.truncated = truncated;
@@ -961,7 +963,7 @@ int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8
     io.conveyor_speed = info->conveyor_speed;
     io.out_of_reach = info->out_of_reach;
     io.force_terminate = info->force_terminate;
-    io.terminal_obs = info->terminal_obs;
+    io.terminal_obs = (float*)info->terminal_obs;
     io.ep_return = info->episode_return;
     io.ep_len = info->episode_length;
     io.terminal_scores = info->terminal_scores;

@@ -140,6 +140,7 @@ struct Model {
                              // kinematics (FM_SERIAL_FK=1); bit 8 = the Newton warmstart's two row passes
                              // (FM_TWO_PASS_SETUP=1)
   int ovf_abort;             // 1: a stage above the contact capacity abandons the env-step (State::rerun), not cut it
+  int obs64;                 // 1: observation rows (obs, terminal_obs) are float64 (fm_config.obs_float64)
 };
 
 template <typename T>

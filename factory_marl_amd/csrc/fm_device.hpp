@@ -51,7 +51,21 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-#define LANE ((int)threadIdx.x)
+// The lane index, opaque at each use: lane-derived values (per-lane LDS offsets, lane masks, LANE / 3, LANE % 9, ...)
+// are recomputed where they are used instead of being hoisted out of the substep loop by the compiler -- hoisted,
+// the (2,4) kernel held ~65 of them live across the whole env-step and spilled them to scratch at two waves per
+// SIMD (a scratch reload per use instead of one VALU op).  FM_OPAQUE_LANE=0: the plain threadIdx.x.
+#ifndef FM_OPAQUE_LANE
+#define FM_OPAQUE_LANE 1
+#endif
+__device__ __forceinline__ int lane_id() {
+  int t = (int)threadIdx.x;
+#if FM_OPAQUE_LANE
+  asm volatile("" : "+v"(t));
+#endif
+  return t;
+}
+#define LANE (::fm::lane_id())
 // A workgroup is exactly one wave.  Lanes hand data to each other through LDS at SYNC(): a
 // wavefront-scope release fence, the wave barrier, a wavefront-scope acquire fence.  The fences order
 // every memory access before the barrier ahead of every access after it (the compiler may not move LDS
@@ -5359,6 +5373,9 @@ __device__ __forceinline__ void task_tail(const Model<T>& M, const Ws<T, DIM>& w
 }
 
 template <typename T, typename DIM>
+// obs: float32 rows, or float64 rows when M.obs64 (the toggle classes' observation is float64 in the reference: the
+// float32 state block concatenated with the float64 IK proposals, environments.py:576 -- numpy widens the float32
+// columns exactly, and the proposals keep all their bits)
 __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w, int32_t* ti, double* td, float* obs) {
   const DIM dm(M.dm);
   const int A = dm.A, K = dm.K;
@@ -5399,9 +5416,17 @@ __device__ __forceinline__ void write_obs(const Model<T>& M, const Ws<T, DIM>& w
       val = k < n ? (float)v[1 + 6 * idx[k] + c] : 0.0f;
     } else {  // IKTogglingEnv: the IK proposals (environments.py:576)
       const int r = e - 24 * A - 13 * K;
-      val = (float)ik_arm(dm, ti, td, r / 8).ik_actions()[r % 8];
+      const double pv = ik_arm(dm, ti, td, r / 8).ik_actions()[r % 8];
+      if (M.obs64) {
+        ((double*)obs)[e] = pv;
+        continue;
+      }
+      val = (float)pv;
     }
-    obs[e] = val;
+    if (M.obs64)
+      ((double*)obs)[e] = (double)val;
+    else
+      obs[e] = val;
   }
 }
 
@@ -5616,7 +5641,7 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
   SYNC();
   FULL_SYNC();
   if (env_toggle(M.env_class)) ik_proposals(M, w, ti, td);  // reset()'s observation (environments.py:245)
-  if (obs) write_obs(M, w, ti, td, obs + (size_t)arena * dm.obs_dim);
+  if (obs) write_obs(M, w, ti, td, obs + (size_t)arena * dm.obs_dim * (M.obs64 ? 2 : 1));
 }
 
 // IK: the env class may compose IK proposals (every class but AllFullRL); the AllFullRL instantiation carries
@@ -5867,7 +5892,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
     // ---- auto-reset (reset_sim, base_env.py:177-198): terminal obs, zero state, TaskManager.reset,
     // then one more pass of this loop = the forward at the reset state that leaves qacc_warmstart
     FULL_SYNC();
-    if (io.terminal_obs) write_obs(M, w, ti, td, io.terminal_obs + (size_t)arena * dm.obs_dim);
+    if (io.terminal_obs) write_obs(M, w, ti, td, io.terminal_obs + (size_t)arena * dm.obs_dim * (M.obs64 ? 2 : 1));
     SYNC();
     for (int i = LANE; i < dm.nq; i += WAVE) w.qd()[i] = 0.0;
     for (int i = LANE; i < dm.nv; i += WAVE) {
@@ -5889,7 +5914,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
   store_state(M, S, w, arena);
   FULL_SYNC();
   if (IK && reset_pass && env_toggle(ec)) ik_proposals(M, w, ti, td);  // reset()'s observation after the auto-reset
-  if (io.obs) write_obs(M, w, ti, td, io.obs + (size_t)arena * dm.obs_dim);
+  if (io.obs) write_obs(M, w, ti, td, io.obs + (size_t)arena * dm.obs_dim * (M.obs64 ? 2 : 1));
   PMARK(PH_TAIL);
   if (M.prof && LANE < PH_LAST) atomicAdd(M.prof + LANE, w.prof()[LANE]);
   {

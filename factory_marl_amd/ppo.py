@@ -80,6 +80,7 @@ class ActorCriticPolicy(nn.Module):
 
     # ------------------------------------------------------------------ distributions
     def _dist_params(self, obs):
+        obs = obs.float()  # SB3 preprocess_obs: Box observations as float32 (the toggle envs' rows are float64)
         lp = self.mlp_extractor.policy_net(obs)
         lv = self.mlp_extractor.value_net(obs)
         return self.action_net(lp), self.value_net(lv).squeeze(-1)
@@ -131,6 +132,7 @@ class ActorCriticPolicy(nn.Module):
         return values, logp, ent
 
     def predict_values(self, obs):
+        obs = obs.float()
         return self.value_net(self.mlp_extractor.value_net(obs)).squeeze(-1)
 
     @torch.no_grad()

@@ -99,7 +99,7 @@ def _specs_from_env_fns(env_fns):
 class FactoryVecEnv:
     def __init__(self, num_envs, env_class="AllFullRLProgressRewardEnv", env_kwargs=None, device=0,
                  precision="fp32", seeds=None, return_numpy=True, max_contacts=0, solver_tolerance=0.0,
-                 solver_iterations=0):
+                 solver_iterations=0, obs_dtype=None):
         import torch
 
         self.torch = torch
@@ -128,6 +128,14 @@ class FactoryVecEnv:
             cfg.solver_tolerance = float(solver_tolerance)
         if solver_iterations > 0:
             cfg.solver_iterations = int(solver_iterations)
+        # observation rows: the reference's IKTogglingEnv returns float64 rows (its float32 state columns concatenated
+        # with the float64 IK proposals, environments.py:576; SubprocVecEnv stacks them as returned -- the saved
+        # runs' _last_obs are float64), every other class float32.  obs_dtype overrides ("float32" / "float64").
+        if obs_dtype is None:
+            obs_dtype = "float64" if env_class in TOGGLE_CLASSES else "float32"
+        if str(obs_dtype) not in ("float32", "float64"):
+            raise ValueError(f"obs_dtype must be float32 or float64, got {obs_dtype!r}")
+        cfg.obs_float64 = 1 if str(obs_dtype) == "float64" else 0
         for k in ["initial_conveyor_speed", "conveyor_acceleration", "pt_time", "force_contact_threshold",
                   "control_frequency", "spawn_freq", "spawn_freq_increase"]:
             setattr(cfg, k, float(kw[k]))
@@ -163,7 +171,9 @@ class FactoryVecEnv:
         self.return_numpy = return_numpy
         dev = self.device
         n = self.num_envs
-        self.obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=dev)
+        odt = torch.float64 if cfg.obs_float64 else torch.float32
+        self.obs_dtype = np.float64 if cfg.obs_float64 else np.float32
+        self.obs = torch.zeros(n, self.obs_dim, dtype=odt, device=dev)
         self.rewards = torch.zeros(n, dtype=torch.float32, device=dev)
         self.terminated = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros(n, dtype=torch.uint8, device=dev)
@@ -173,7 +183,7 @@ class FactoryVecEnv:
         self.conveyor_speed = torch.zeros(n, dtype=torch.float64, device=dev)
         self.out_of_reach = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.force_terminate = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.terminal_obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=dev)
+        self.terminal_obs = torch.zeros(n, self.obs_dim, dtype=odt, device=dev)
         self.ep_return = torch.zeros(n, dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
         self.terminal_scores = torch.zeros(n, 2, dtype=torch.int32, device=dev)

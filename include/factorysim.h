@@ -75,6 +75,9 @@ typedef struct fm_config {
   double base_reward;
   int32_t solver_iterations; /* Newton iterations cap (MuJoCo default 100) */
   double solver_tolerance;   /* scaled improvement / gradient tolerance (MuJoCo default 1e-8) */
+  int32_t obs_float64;       /* 1: obs / terminal_obs rows are float64 (the toggle classes' observation dtype in the
+                                reference: float32 state columns widened, float64 IK proposals, environments.py:576);
+                                0: float32 rows (default) */
 } fm_config;
 
 /* Per-step info, all DEVICE pointers, any may be NULL (info dict of base_env.py:274-280 plus the
@@ -86,7 +89,8 @@ typedef struct fm_info {
   double* conveyor_speed;   /* [N] */
   uint8_t* out_of_reach;    /* [N]   TaskManager.terminate */
   uint8_t* force_terminate; /* [N] */
-  float* terminal_obs;      /* [N, obs_dim] written for arenas that terminated (before auto-reset) */
+  void* terminal_obs;       /* [N, obs_dim] float32 (float64 with obs_float64) written for arenas that terminated
+                             (before auto-reset) */
   double* episode_return;   /* [N]   Monitor "r" of the finished episode (valid where terminated) */
   int32_t* episode_length;  /* [N]   Monitor "l" */
   int32_t* terminal_scores; /* [N, 2] scores of the finished episode (ep_score_history entry) */
@@ -131,12 +135,12 @@ int fm_workspace_bytes(const fm_handle* h); /* LDS bytes of one arena's env-step
 /* reset(): reset arenas where mask[i] != 0 (device uint8 [N]; NULL = all) and write their obs.
  * Mirrors BaseEnv.reset_sim + FactoryManipulationEnv.reset (environments.py:204-248): the
  * TaskManager RNG is NOT reseeded (task_utils.py:19), progress-reward distance memories persist. */
-int fm_reset(fm_handle* h, const uint8_t* mask, float* obs);
+int fm_reset(fm_handle* h, const uint8_t* mask, void* obs);
 
-/* step(): actions float32 [N, act_dim] (device).  Writes obs [N, obs_dim] (reset obs for arenas
- * that terminated), reward [N], terminated [N], truncated [N] (always 0: the reference has no
- * time limit, environments.py:202), and info.  Any output pointer may be NULL. */
-int fm_step(fm_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated,
+/* step(): actions float32 [N, act_dim] (device).  Writes obs [N, obs_dim] (float32, or float64 with
+ * cfg.obs_float64; reset obs for arenas that terminated), reward [N], terminated [N], truncated [N] (always 0: the
+ * reference has no time limit, environments.py:202), and info.  Any output pointer may be NULL. */
+int fm_step(fm_handle* h, const float* actions, void* obs, float* reward, uint8_t* terminated,
             uint8_t* truncated, const fm_info* info);
 
 /* Teacher forcing / checkpointing of the full arena state (HOST buffers).

@@ -11,6 +11,10 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
+import pathlib  # noqa: E402
+
+_FIX = pathlib.Path(__file__).resolve().parent / "golden" / "runs_fixtures.npz"
+
 
 def _have_gpu():
     return torch.cuda.is_available()
@@ -29,6 +33,11 @@ def test_learning_py_make_vec_env_line_on_gpu():
                        n_envs=CONFIG["num_envs"], vec_env_cls=FactoryVecEnv)
     obs = env.reset()
     assert isinstance(obs, np.ndarray) and obs.shape == (8, 24 * 4 + 13 * 10 + 8 * 4)
+    # the toggle classes' rows are float64 as in the reference (environments.py:576; the saved run y6lp1j7k's
+    # SB3 _last_obs is float64 [8, 258], tests/golden/runs_fixtures.npz)
+    fx = np.load(_FIX, allow_pickle=False)
+    ref = fx["last_obs_y6lp1j7k"]
+    assert obs.dtype == np.float64 and ref.dtype == obs.dtype and ref.shape == obs.shape
     assert env.action_space.nvec.tolist() == [2] * 4
     rng = np.random.default_rng(0)
     for _ in range(5):
@@ -37,6 +46,43 @@ def test_learning_py_make_vec_env_line_on_gpu():
     assert all("scores" in i for i in infos)
     assert env.get_attr("ep_score_history") == [[] for _ in range(8)] or len(env.get_attr("ep_score_history")) == 8
     env.close()
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("env_class", ["PauseIKToggleEnv", "BackupIKToggleEnv"])
+def test_toggle_observation_rows_are_float64(env_class):
+    """IKTogglingEnv._process_observation (environments.py:560-577) concatenates the float32 state columns with the
+    float64 IK proposals: the GPU env's rows are float64, the state columns are the float32 values widened exactly,
+    the proposal columns carry the arena record's float64 ik_actions bit for bit; obs_dtype="float32" gives the
+    rounded rows"""
+    from factory_marl_amd import FactoryVecEnv, state as st
+    from factory_marl_amd.environments import run_kwargs
+
+    n, A, K = 16, 2, 4
+    kw = run_kwargs(env_class, num_arms=A, max_num_objects=K, seed=42)
+    e64 = FactoryVecEnv(n, env_class=env_class, env_kwargs=kw, return_numpy=False)
+    e32 = FactoryVecEnv(n, env_class=env_class, env_kwargs=kw, return_numpy=False, obs_dtype="float32")
+    for e in (e64, e32):
+        e.reset()
+    g = torch.Generator(device=e64.device)
+    g.manual_seed(5)
+    for _ in range(30):
+        a = (torch.rand(n, A, device=e64.device, generator=g) < 0.5).float()
+        o64 = e64.step_tensors(a)[0].clone()
+        o32 = e32.step_tensors(a)[0].clone()
+    assert o64.dtype == torch.float64 and o32.dtype == torch.float32
+    o64, o32 = o64.cpu().numpy(), o32.cpu().numpy()
+    ns = 24 * A + 13 * K
+    assert np.array_equal(o64[:, :ns], o32[:, :ns].astype(np.float64))  # widened float32 columns
+    assert np.array_equal(o64[:, ns:].astype(np.float32), o32[:, ns:])
+    recs = e64.get_state()
+    for i in range(n):
+        d, _, _ = st.unpack(A, K, recs[i])
+        ik = np.array([d[len(d) - 27 * A + 27 * a + 11 + j] for a in range(A) for j in range(8)])
+        assert np.array_equal(o64[i, ns:], ik)  # the float64 proposals, unrounded
+    assert np.abs(o64[:, ns:] - o64[:, ns:].astype(np.float32)).max() > 0  # they do carry bits beyond float32
+    e64.close()
+    e32.close()
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
