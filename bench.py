@@ -393,34 +393,7 @@ def main():
                 "ms_per_step": round(w64 / args.fp64_steps * 1e3, 4), "kernel_ms_avg": round(k64, 4),
                 "diagnostics": diagnostics(dc64, N, args.fp64_steps)}
     if ctx.rank == 0:
-        B = algorithmic_bytes(A, K)
-        achieved = N * B / (kern_ms * 1e-3) / 1e9
-        tj = load_json(args.traffic_json) or {}
-        traffic = None
-        if tj.get("arenas") == N and tj.get("precision") == args.precision and tj.get("A") == A and tj.get("K") == K:
-            traffic = tj.get("hbm_bytes_per_launch")
-        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
-                "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
-                "algorithmic_bytes_per_arena_step": B,
-                "binding": "neither HBM nor MFMA: dependent LDS / VALU / L2 latency chains, two waves (arenas) per SIMD"}
-        if traffic is not None:
-            roof["traffic_note"] = ("PMC TCC -> memory-fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE): the per-arena "
-                                    "scratch blocks (contact records, Hessian) and register spills that leave the L2, "
-                                    "whether the MALL or HBM serves them; %.1f %% of the HBM peak at this launch time"
-                                    % (100.0 * traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS))
-        vj = load_json(args.valu_json) or {}
-        if vj.get("A") == A and vj.get("K") == K and vj.get("precision") == args.precision:
-            flops = vj["valu_lane_flops_per_arena_step"] * N
-            vinst = vj["valu_wave_instr_per_arena_step"] * N
-            t = kern_ms * 1e-3
-            peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else FP64_PEAK_TFLOPS
-            roof["valu"] = {"achieved": round(flops / t / 1e12, 4), "peak": peak, "unit": "TFLOP/s",
-                            "frac": round(flops / t / 1e12 / peak, 5),
-                            "issue_frac": round(vinst * 2 / (t * 2.4e9 * 256 * 4), 5),
-                            "note": "lane FLOPs of executed fp32 VALU instructions (all 64 lanes counted) and "
-                                    "VALU issue cycles (2 per wave-instruction) over the chip's SIMD-cycles at "
-                                    "2.4 GHz; counts per arena env-step from " + os.path.relpath(args.valu_json, ROOT)}
+        roof = make_roofline(args, N, A, K, kern_ms, args.traffic_json, args.valu_json)
         line = {
             "metric": "env-steps/sec (whole node), 4096 arenas 2-arm×4-obj; 1/2/4/8 MI355X",
             "value": round(value, 2),
@@ -450,6 +423,52 @@ def main():
             line["cpu_baseline"] = cpu_baseline(A, K, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     ctx.close()
+
+
+def make_roofline(args, N, A, K, kern_ms, traffic_json, valu_json):
+    """the line's roofline block for the dominant kernel (the env-step kernel): SURVEY §8(d)'s algorithmic bytes per
+    arena env-step x the arenas of one launch / the kernel's event-timed average launch (fm_get_kernel_time), the PMC
+    memory-fabric traffic per launch and the VALU work (profiles/, rocprofv3 passes) when they were taken on this
+    workload"""
+    B = algorithmic_bytes(A, K)
+    achieved = N * B / (kern_ms * 1e-3) / 1e9
+    tj = load_json(traffic_json) or {}
+    traffic = None
+    if tj.get("arenas") == N and tj.get("precision") == args.precision and tj.get("A") == A and tj.get("K") == K:
+        traffic = tj.get("hbm_bytes_per_launch")
+    roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
+            "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
+            "algorithmic_bytes_per_arena_step": B,
+            "binding": "neither HBM nor MFMA: dependent LDS / VALU / L2 latency chains, two waves (arenas) per SIMD"}
+    if traffic is not None:
+        roof["traffic_note"] = ("PMC TCC -> memory-fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE): the per-arena "
+                                "scratch blocks (contact records, Hessian) and register spills that leave the L2, "
+                                "whether the MALL or HBM serves them; %.1f %% of the HBM peak at this launch time"
+                                % (100.0 * traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS))
+    vj = load_json(valu_json) or {}
+    if vj.get("A") == A and vj.get("K") == K and vj.get("precision") == args.precision:
+        flops = vj["valu_lane_flops_per_arena_step"] * N
+        vinst = vj["valu_wave_instr_per_arena_step"] * N
+        t = kern_ms * 1e-3
+        peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else FP64_PEAK_TFLOPS
+        frac = flops / t / 1e12 / peak
+        note = "lane FLOPs of executed fp32 VALU instructions (all 64 lanes counted)"
+        if "valu_lane_flops_f64_per_arena_step" in vj and vj.get("valu_lane_flops_f64_per_arena_step", 0) > 0 \
+                and args.precision == "fp32":
+            # the fp32 build's float64 work (master state, narrowphase, Newton iterate) runs at half the fp32 rate:
+            # the fraction is the share of the VALU peak's time the two kinds of FLOPs take together
+            f32 = vj["valu_lane_flops_f32_per_arena_step"] * N
+            f64 = vj["valu_lane_flops_f64_per_arena_step"] * N
+            frac = (f32 / FP32_PEAK_TFLOPS + f64 / FP64_PEAK_TFLOPS) / t / 1e12
+            note = ("lane FLOPs of executed fp32 + fp64 VALU instructions (all 64 lanes counted; fp64 priced at its "
+                    "half rate in frac)")
+        roof["valu"] = {"achieved": round(flops / t / 1e12, 4), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(frac, 5),
+                        "issue_frac": round(vinst * 2 / (t * 2.4e9 * 256 * 4), 5),
+                        "note": note + " and VALU issue cycles (2 per wave-instruction) over the chip's SIMD-cycles at "
+                                "2.4 GHz; counts per arena env-step from " + os.path.relpath(valu_json, ROOT)}
+    return roof
 
 
 def main_config5(args):
@@ -483,6 +502,8 @@ def main_config5(args):
                        "arenas_per_gpu": N, "num_arms": A, "max_num_objects": K,
                        "parallelism": f"arena-sharded x{ctx.world} (no collective)"},
             "kernel_ms_avg": round(kern_ms, 4),
+            "roofline": make_roofline(args, N, A, K, kern_ms, os.path.join(ROOT, "profiles", "pmc5_traffic.json"),
+                                      os.path.join(ROOT, "profiles", "pmc5_valu.json")),
             "diagnostics": diagnostics(dc, N, args.steps),
         }
         if ctx.world > 1:

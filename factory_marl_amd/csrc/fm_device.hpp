@@ -58,6 +58,12 @@ __device__ __forceinline__ void static_for(F&& f) {
 #ifndef FM_OPAQUE_LANE
 #define FM_OPAQUE_LANE 1
 #endif
+// a uniform int the compiler must re-read at each use (not hoisted: see the record macros of step_arena)
+__device__ __forceinline__ int opaque_uniform(int x) {
+  x = __builtin_amdgcn_readfirstlane(x);  // uniform by contract (one arena per wave)
+  asm volatile("" : "+s"(x));
+  return x;
+}
 __device__ __forceinline__ int lane_id() {
   int t = (int)threadIdx.x;
 #if FM_OPAQUE_LANE
@@ -5679,11 +5685,14 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
     w.misc()[MISC_CMAX] = 0;
     w.misc()[MISC_MC_OK] = 0;  // the cached midphase list is rebuilt at the first substep of every launch
   }
-#define ti (S.ints + (size_t)arena * dm.int_stride)
-#define td (S.dbl + (size_t)arena * dm.dbl_stride + nu)  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
-#define rng (S.rng + 4 * (size_t)arena)
-#define ctr (S.counters + FM_NCTR * (size_t)arena)
-#define act (io.actions + (size_t)arena * dm.act_dim)
+  // the arena's record addresses, recomputed at each use from an opaque copy of the arena index (hoisted, the 64-bit
+  // offsets stay live across the substep loop and spill)
+#define ARENA_ (::fm::opaque_uniform(arena))
+#define ti (S.ints + (size_t)ARENA_ * dm.int_stride)
+#define td (S.dbl + (size_t)ARENA_ * dm.dbl_stride + nu)  // spawn_freq, speed, play_time, grip[A], bucket[A], ret
+#define rng (S.rng + 4 * (size_t)ARENA_)
+#define ctr (S.counters + FM_NCTR * (size_t)ARENA_)
+#define act (io.actions + (size_t)ARENA_ * dm.act_dim)
   if constexpr (IK && (can_abandon || DIM::rerun)) {
     // the IK compose below writes the FSM / last-action blocks of the task records: keep the step's starting
     // records for a rerun (the rerun restores them first)
@@ -5772,7 +5781,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
   load_state(M, S, w, arena, true);
   SYNC();
 #define lp (0.001 / (0.001 + M.pt_time))
-#define phw (S.phys + (size_t)arena * dm.phys_stride)
+#define phw (S.phys + (size_t)ARENA_ * dm.phys_stride)
 #define sc_ (w.scal())  // [0] reward, [1] terminated, [2] out_of_reach, [3] force_terminate
   bool reset_pass = false;
   // Every physics phase has exactly one call site (the kernel is one loop), which keeps the code that a
@@ -5936,6 +5945,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
 #undef act
 #undef phw
 #undef lp
+#undef ARENA_
 }
 
 template <typename T, typename DIM, bool IK>

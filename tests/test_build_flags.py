@@ -88,3 +88,17 @@ def test_step_kernels_have_a_fixed_private_segment():
     ks = {k: v for k, v in meta.items() if "step_kernel" in k[1]}
     assert ks
     assert not [k for k, v in ks.items() if v.get("uses_dynamic_stack")], ks
+
+
+def test_benchmark_kernel_does_not_spill():
+    """the config-2 kernel (step_kernel<float, FixedDims<2, 4>, AllFullRL>) is register-allocated for two waves per
+    SIMD (256 registers per lane) without VGPR spills and without a private segment: round 4 spilled 180 VGPRs
+    (660 B of scratch per lane, ~20 GB of memory-fabric traffic per launch); hoisted lane- and arena-derived values
+    were the spill set (fm_device.hpp lane_id / opaque_uniform)"""
+    _, meta = _scan()
+    k = [(co, n, v) for (co, n), v in meta.items()
+         if n.startswith("void fm::step_kernel<float, fm::FixedDims<2, 4, false>, false>")]
+    assert len(k) == 1, k
+    v = k[0][2]
+    assert v["vgpr_spill_count"] == 0 and v["private_segment_fixed_size"] == 0, v
+    assert v["vgpr_count"] + v.get("agpr_count", 0) <= 256, v

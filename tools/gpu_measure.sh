@@ -80,13 +80,46 @@ for l in open('$O/$step$S.jsonl'):
       timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 \
         SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d $O/pmc_valu$S -- python3 \
         bench.py $P > $O/pmc_valu$S.log 2>&1 || fail pmc_valu $? $O/pmc_valu$S.log
+      timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
+        SQ_INSTS_VALU_TRANS_F64 SQ_WAVES --output-format csv -d $O/pmc_valu64$S -- python3 \
+        bench.py $P > $O/pmc_valu64$S.log 2>&1 || fail pmc_valu64 $? $O/pmc_valu64$S.log
       F=$(find $O/pmc_fetch$S -name "*counter_collection.csv" | head -1)
       W=$(find $O/pmc_write$S -name "*counter_collection.csv" | head -1)
       V=$(find $O/pmc_valu$S -name "*counter_collection.csv" | head -1)
+      V64=$(find $O/pmc_valu64$S -name "*counter_collection.csv" | head -1)
       Q=$(find $O/pmc_sq$S -name "*counter_collection.csv" | head -1)
       python tools/pmc_traffic.py $F $W --arenas 4096 --out $O/pmc_traffic$S.json || fail traffic $?
-      python tools/pmc_valu.py $V --arenas 4096 --last 3 --out $O/pmc_valu$S.json || fail valu $?
+      python tools/pmc_valu.py $V --f64 $V64 --arenas 4096 --last 3 --out $O/pmc_valu$S.json || fail valu $?
       python tools/pmc_sq.py $Q $O/pmc_sq_summary$S.json || fail sq $? ;;
+    ktrace5|pmc5)
+      # config 5's kernel ((4,16) PauseIKToggleEnv fp32, 4096 arenas on one GPU): kernel stats, then the PMC passes
+      P5="--workload config5 --steps 3 --warmup 1 --no-cpu-baseline"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace5$S -- python3 bench.py \
+        --workload config5 --steps 8 --warmup 2 --no-cpu-baseline > $O/ktrace5$S.log 2>&1 || fail ktrace5 $? $O/ktrace5$S.log
+      find $O/ktrace5$S -name "*kernel_stats.csv" | head -1 | xargs -r head -4
+      if [ $step = pmc5 ]; then
+        timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc5_fetch$S -- python3 bench.py $P5 \
+          > $O/pmc5_fetch$S.log 2>&1 || fail pmc5_fetch $? $O/pmc5_fetch$S.log
+        timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc5_write$S -- python3 bench.py $P5 \
+          > $O/pmc5_write$S.log 2>&1 || fail pmc5_write $? $O/pmc5_write$S.log
+        timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+          SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $O/pmc5_sq$S -- python3 bench.py $P5 \
+          > $O/pmc5_sq$S.log 2>&1 || fail pmc5_sq $? $O/pmc5_sq$S.log
+        timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 \
+          SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d $O/pmc5_valu$S -- python3 \
+          bench.py $P5 > $O/pmc5_valu$S.log 2>&1 || fail pmc5_valu $? $O/pmc5_valu$S.log
+        timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
+          SQ_INSTS_VALU_TRANS_F64 SQ_WAVES --output-format csv -d $O/pmc5_valu64$S -- python3 \
+          bench.py $P5 > $O/pmc5_valu64$S.log 2>&1 || fail pmc5_valu64 $? $O/pmc5_valu64$S.log
+        python tools/pmc_traffic.py $(find $O/pmc5_fetch$S -name "*counter_collection.csv" | head -1) \
+          $(find $O/pmc5_write$S -name "*counter_collection.csv" | head -1) --arenas 4096 --arms 4 --objects 16 \
+          --out $O/pmc5_traffic$S.json || fail traffic5 $?
+        python tools/pmc_valu.py $(find $O/pmc5_valu$S -name "*counter_collection.csv" | head -1) \
+          --f64 $(find $O/pmc5_valu64$S -name "*counter_collection.csv" | head -1) --arenas 4096 --arms 4 --objects 16 \
+          --last 2 --out $O/pmc5_valu$S.json || fail valu5 $?
+        python tools/pmc_sq.py $(find $O/pmc5_sq$S -name "*counter_collection.csv" | head -1) $O/pmc5_sq_summary$S.json \
+          || fail sq5 $?
+      fi ;;
     phase24)
       timeout -k 10 200 python tools/phase_profile.py --precision fp32 > $O/phase_fp32$S.json 2> $O/phase$S.err \
         || fail phase24 $? $O/phase$S.err ;;
