@@ -249,7 +249,7 @@ struct Lay {
   int bc;     // T [64]       broadcast row of the register-resident Cholesky
   int mcache, mpos;  // cached midphase: uint32 [mc_cap(nv)] hit list, T [ncb][3] body positions at the build
   int bposd, bRd;    // fp32 scenes with DIM::f64arms: double [A][10][3], [A][10][9] arm body poses (narrowphase)
-  int tblk;          // fp32 (2,8), (2,10), (4,16): the tree-block Newton solve's workspace (TB_*; Newton phase)
+  int tblk;          // (2,8), (2,10), (4,16), (2,4) wide: the tree-block Newton solve's workspace (T, TB_*; Newton phase)
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -573,7 +573,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.g = take(8 * nv);
   L.Ma = take(8 * nv);
   L.tmp = take(8 * nv);
-  if (treeblk) L.tblk = take(4 * tb_floats(ntree));
+  if (treeblk) L.tblk = take(tsize * tb_floats(ntree));
   int uend = off;
   off = u0;
   L.gx = take(tsize * 4 * ngc);
@@ -688,7 +688,7 @@ struct FixedDims {
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
     return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms,
-                       gl_lists, treeblk && TS == 4);
+                       gl_lists, treeblk);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -180,12 +180,12 @@ struct Ws {
       return (double*)(base + L->tmp);
     }
   }
-  __device__ __forceinline__ float* tblk() const {
+  __device__ __forceinline__ T* tblk() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (float*)(base + c.tblk);
+      return (T*)(base + c.tblk);
     } else {
-      return (float*)(base + L->tblk);
+      return (T*)(base + L->tblk);
     }
   }
   __device__ __forceinline__ T* fa() const {
@@ -3897,48 +3897,57 @@ __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const 
 // chol_solve_reg for the tree-block solve's small coupled system (fp32, n <= NVM): the same factor, but the pivot
 // column reaches the other lanes by v_readlane (lane i holds L[i][k] after the scaling) instead of an LDS row and two
 // wave barriers per pivot -- the system is one small dense block solved once per Newton iteration
-template <int NVM>
-__device__ __forceinline__ void chol_solve_rl(const float* H, int nv, const double* g, float* dir) {
+// (T = double: the fp64 tree-block solve; the pivot broadcasts go through lane_bcast, ds_bpermute for 64-bit values
+// -- see the 64-bit cross-lane hazard)
+template <typename T>
+__device__ __forceinline__ T rsqrt_div(T d) {
+  if constexpr (sizeof(T) == 4)
+    return 1.0f / sqrtf(d);
+  else
+    return 1.0 / sqrt(d);
+}
+template <int NVM, typename T = float>
+__device__ __forceinline__ void chol_solve_rl(const T* H, int nv, const double* g, T* dir) {
   const int j = LANE;
-  const float tiny = 1e-37f;
-  float col[NVM];
+  const T tiny = sizeof(T) == 4 ? T(1e-37f) : T(1e-300);
+  T col[NVM];
 #pragma unroll
-  for (int i = 0; i < NVM; i++) col[i] = (i < nv && j < nv) ? H[i * nv + j] : 0.0f;
+  for (int i = 0; i < NVM; i++) col[i] = (i < nv && j < nv) ? H[i * nv + j] : T(0);
   SYNC();
-  float dinv = 1.0f;
+  T dinv = T(1);
 #pragma unroll
   for (int k = 0; k < NVM; k++) {
     if (k < nv) {
-      float d = readlane(col[k], k);
+      T d = lane_bcast(col[k], k);
       d = d > tiny ? d : tiny;
-      const float ri = 1.0f / sqrtf(d);
-      const float lj = col[k] * ri;  // lane j > k: L[j][k]; lane k: L[k][k]
+      const T ri = rsqrt_div(d);
+      const T lj = col[k] * ri;  // lane j > k: L[j][k]; lane k: L[k][k]
       if (j == k) dinv = ri;
       if (j >= k) col[k] = lj;
-      float lv[NVM];
+      T lv[NVM];
 #pragma unroll
-      for (int i = k + 1; i < NVM; i++) lv[i] = readlane(lj, i);
+      for (int i = k + 1; i < NVM; i++) lv[i] = lane_bcast(lj, i);
       if (j > k) {
 #pragma unroll
         for (int i = k + 1; i < NVM; i++) col[i] -= lv[i] * lj;
       }
     }
   }
-  float acc = j < nv ? (float)-g[j] : 0.0f;
-  float y = 0.0f;
+  T acc = j < nv ? (T)-g[j] : T(0);
+  T y = T(0);
 #pragma unroll
   for (int k = 0; k < NVM; k++) {
     if (k < nv) {
-      const float yk = readlane(acc * dinv, k);
+      const T yk = lane_bcast(acc * dinv, k);
       if (j == k) y = yk;
       if (j > k) acc -= col[k] * yk;
     }
   }
-  float acc2 = y, x = 0.0f;
+  T acc2 = y, x = T(0);
 #pragma unroll
   for (int k = NVM - 1; k >= 0; k--) {
     if (k < nv) {
-      const float xk = readlane(acc2 * dinv, k);
+      const T xk = lane_bcast(acc2 * dinv, k);
       if (j == k) x = xk;
       if (j < k) acc2 -= col[k] * dinv * xk;
     }
@@ -4311,7 +4320,7 @@ __device__ constexpr bool pc_scene() {
 
 template <typename T, typename DIM>
 __device__ constexpr bool treeblk_scene() {
-  if constexpr (DIM::fixed && sizeof(T) == 4)
+  if constexpr (DIM::fixed)
     return DIM::treeblk;
   else
     return false;
@@ -4321,9 +4330,9 @@ __device__ __forceinline__ unsigned wave_or_u32(unsigned x) {
   for (int o = 32; o > 0; o >>= 1) x |= (unsigned)__shfl_xor((int)x, o);
   return x;
 }
-template <typename DIM>
-__device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<float, DIM>& w, const double* g,
-                                               float* dir, int ncon, int nrow) {
+template <typename T, typename DIM>
+__device__ __forceinline__ bool newton_treeblk(const Model<T>& M, const Ws<T, DIM>& w, const double* g, T* dir,
+                                               int ncon, int nrow) {
   constexpr int NT = DIM::ntree, KK = DIM::K;
   static_assert(NT <= 32 && DIM::nv <= 1 + 9 * (NT - 1), "one 32-bit tree mask; trees of <= 9 dofs");
   const DIM dm(M.dm);
@@ -4351,8 +4360,8 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
     const unsigned below = cm & ((1u << t) - 1u);
     return 6 * __popc(below & CUBES) + 9 * __popc(below & ~CUBES);
   };
-  float* const tbw = w.tblk();
-  float* const R = tbw + tb_rest(NT);
+  T* const tbw = w.tblk();
+  T* const R = tbw + tb_rest(NT);
   int* const cmap = (int*)(tbw + tb_map(NT));
   // ---- zero the blocks, belt rows and the coupled system; the coupled system's position map
   for (int e = LANE; e < TB_BLK * NT; e += WAVE) tbw[e] = 0.0f;
@@ -4365,11 +4374,11 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
   // ---- mass matrix: belt and cube diagonals, arm blocks (lower triangles)
   for (int d = LANE; d < dm.nv; d += WAVE) {
     const int t = dof_tree(dm, d), i = d - tree_dof(dm, t);
-    float* B = tbw + TB_BLK * t;
+    T* B = tbw + TB_BLK * t;
     if (t <= KK) {
       B[P9(i, i)] = Mdiag(M, w, d);
     } else {
-      const float* Mr = w.Marm() + 81 * (t - 1 - KK) + 9 * i;
+      const T* Mr = w.Marm() + 81 * (t - 1 - KK) + 9 * i;
       for (int j = 0; j <= i; j++) B[P9(i, j)] = Mr[j];
     }
   }
@@ -4377,13 +4386,13 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
   // ---- contacts: one lane per contact
   for (int c = LANE; c < ncon; c += WAVE) {
     const int* ci = w.ci() + 4 * c;
-    const float* cr = w.cr() + CR_N * c;
-    const float* Kc = cr + CR_K;
-    const float k0 = Kc[0], k1 = Kc[1], k2 = Kc[2], k3 = Kc[3], k4 = Kc[4], k5 = Kc[5];
-    if (k0 == 0.0f) continue;  // no active pyramid edge: no Hessian term
+    const T* cr = w.cr() + CR_N * c;
+    const T* Kc = cr + CR_K;
+    const T k0 = Kc[0], k1 = Kc[1], k2 = Kc[2], k3 = Kc[3], k4 = Kc[4], k5 = Kc[5];
+    if (k0 == T(0)) continue;  // no active pyramid edge: no Hessian term
     const int ta = ci[1], tb = ci[2], nda = (ci[3] >> 20) & 15, ndb = (ci[3] >> 24) & 15;
-    const float* J = cr + CR_J;
-    float ja[3][9], jb[3][9], qa[3][9], qb[3][9];
+    const T* J = cr + CR_J;
+    T ja[3][9], jb[3][9], qa[3][9], qb[3][9];
 #pragma unroll
     for (int i = 0; i < 9; i++) {
 #pragma unroll
@@ -4400,7 +4409,7 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
     }
     // own blocks of the two trees (a tree < 0 is the world: no columns)
     if (ta >= 0) {
-      float* B = tbw + TB_BLK * ta;
+      T* B = tbw + TB_BLK * ta;
 #pragma unroll
       for (int i = 0; i < 9; i++)
 #pragma unroll
@@ -4408,7 +4417,7 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
           if (i < nda) atomicAdd(B + P9(i, j), qa[0][i] * ja[0][j] + qa[1][i] * ja[1][j] + qa[2][i] * ja[2][j]);
     }
     if (tb >= 0) {
-      float* B = tbw + TB_BLK * tb;
+      T* B = tbw + TB_BLK * tb;
 #pragma unroll
       for (int i = 0; i < 9; i++)
 #pragma unroll
@@ -4419,21 +4428,21 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
     // cross term B_a' K B_b: a belt row, a contact inside one tree, or an entry pair of the coupled system
     if (tb == 0 || ta == 0) {
       const bool bb = tb == 0;  // the belt is tree b: tree a's belt row, else tree b's
-      float* Bl = tbw + TB_BLK * (bb ? ta : tb) + 45;
+      T* Bl = tbw + TB_BLK * (bb ? ta : tb) + 45;
 #pragma unroll
       for (int i = 0; i < 9; i++) {
-        const float v = bb ? qa[0][i] * jb[0][0] + qa[1][i] * jb[1][0] + qa[2][i] * jb[2][0]
+        const T v = bb ? qa[0][i] * jb[0][0] + qa[1][i] * jb[1][0] + qa[2][i] * jb[2][0]
                            : qb[0][i] * ja[0][0] + qb[1][i] * ja[1][0] + qb[2][i] * ja[2][0];
         if (i < (bb ? nda : ndb)) atomicAdd(Bl + i, v);
       }
     } else if (ta == tb) {
-      float* B = tbw + TB_BLK * ta;
+      T* B = tbw + TB_BLK * ta;
 #pragma unroll
       for (int i = 0; i < 9; i++)
 #pragma unroll
         for (int k = 0; k < 9; k++) {
-          const float v = qa[0][i] * jb[0][k] + qa[1][i] * jb[1][k] + qa[2][i] * jb[2][k];
-          if (i < nda && k < ndb) atomicAdd(B + (i >= k ? P9(i, k) : P9(k, i)), i == k ? 2.0f * v : v);
+          const T v = qa[0][i] * jb[0][k] + qa[1][i] * jb[1][k] + qa[2][i] * jb[2][k];
+          if (i < nda && k < ndb) atomicAdd(B + (i >= k ? P9(i, k) : P9(k, i)), i == k ? T(2) * v : v);
         }
     } else {
       const int ca = cbase(ta), cb = cbase(tb);
@@ -4441,7 +4450,7 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
       for (int i = 0; i < 9; i++)
 #pragma unroll
         for (int k = 0; k < 9; k++) {
-          const float v = qa[0][i] * jb[0][k] + qa[1][i] * jb[1][k] + qa[2][i] * jb[2][k];
+          const T v = qa[0][i] * jb[0][k] + qa[1][i] * jb[1][k] + qa[2][i] * jb[2][k];
           if (i < nda && k < ndb) {
             atomicAdd(R + (ca + i) * n + cb + k, v);
             atomicAdd(R + (cb + k) * n + ca + i, v);
@@ -4452,45 +4461,45 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
   // ---- generic rows (gripper equality, joint limits: inside one tree), one lane per row
   for (int r = LANE; r < nrow; r += WAVE) {
     const int* ri = w.ri() + 4 * r;
-    const float* rr = w.rr() + RR_N * r;
+    const T* rr = w.rr() + RR_N * r;
     if (!(ri[2] == 0 || *dslot(rr, RR_JAR) < 0.0)) continue;
-    const float D = rr[RR_D], c0 = rr[RR_C0], c1 = rr[RR_C1];
+    const T D = rr[RR_D], c0 = rr[RR_C0], c1 = rr[RR_C1];
     const int d0 = ri[0], d1 = ri[1], t = dof_tree(dm, d0), o = tree_dof(dm, t);
-    float* B = tbw + TB_BLK * t;
+    T* B = tbw + TB_BLK * t;
     const int l0 = d0 - o;
     atomicAdd(B + P9(l0, l0), D * c0 * c0);
     if (d1 >= 0) {
       const int l1 = d1 - o;
       atomicAdd(B + P9(l1, l1), D * c1 * c1);
-      atomicAdd(B + (l0 >= l1 ? P9(l0, l1) : P9(l1, l0)), (l0 == l1 ? 2.0f : 1.0f) * D * c0 * c1);
+      atomicAdd(B + (l0 >= l1 ? P9(l0, l1) : P9(l1, l0)), (l0 == l1 ? T(2) : T(1)) * D * c0 * c1);
     }
   }
   SYNC();
   PMARK(PH_NHESS);
   // ---- single trees: lane t factors its block, its belt row and its forward solve in registers
-  const float tiny = 1e-37f;
+  const T tiny = sizeof(T) == 4 ? T(1e-37f) : T(1e-300);
   const int t = LANE;
   const bool single = t > 0 && t < NT && !((cm >> t) & 1u);
   const bool cube = t <= KK;
   const int d0 = t < NT ? tree_dof(dm, t) : 0;
-  float Lb[45], dv[9], lb[9], y[9];
-  float s_t = 0.0f, ly_t = 0.0f;
+  T Lb[45], dv[9], lb[9], y[9];
+  T s_t = T(0), ly_t = T(0);
   if (single) {
-    const float* B = tbw + TB_BLK * t;
+    const T* B = tbw + TB_BLK * t;
 #pragma unroll
     for (int k = 0; k < 45; k++) Lb[k] = B[k];
 #pragma unroll
     for (int k = 0; k < 9; k++) lb[k] = B[45 + k];
     if (cube) {  // identity padding of the cube's 6 x 6 block (its rows 6..8 and belt entries 6..8 are zero)
-      Lb[P9(6, 6)] = 1.0f;
-      Lb[P9(7, 7)] = 1.0f;
-      Lb[P9(8, 8)] = 1.0f;
+      Lb[P9(6, 6)] = T(1);
+      Lb[P9(7, 7)] = T(1);
+      Lb[P9(8, 8)] = T(1);
     }
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-      float d = Lb[P9(k, k)];
+      T d = Lb[P9(k, k)];
       d = d > tiny ? d : tiny;
-      const float ri = 1.0f / sqrtf(d);
+      const T ri = rsqrt_div(d);
       dv[k] = ri;
 #pragma unroll
       for (int i = k + 1; i < 9; i++) Lb[P9(i, k)] *= ri;
@@ -4501,7 +4510,7 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
     }
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-      float a = lb[i], b = (cube && i >= 6) ? 0.0f : (float)-g[d0 + (i < 9 ? i : 0)];
+      T a = lb[i], b = (cube && i >= 6) ? T(0) : (T)-g[d0 + (i < 9 ? i : 0)];
 #pragma unroll
       for (int k = 0; k < i; k++) {
         a -= Lb[P9(i, k)] * lb[k];
@@ -4513,10 +4522,10 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
       ly_t += lb[i] * y[i];
     }
   }
-  const float S = wave_sum(s_t), LY = wave_sum(ly_t);
+  const T S = wave_sum(s_t), LY = wave_sum(ly_t);
   // ---- the coupled system + belt (position m), in LDS with row stride n
   double* const grest = (double*)(tbw + tb_rhs(NT));  // right-hand side (chol_solve_reg negates it)
-  float* const xr = tbw + tb_sol(NT);                  // its solution
+  T* const xr = tbw + tb_sol(NT);                  // its solution
   for (int e = LANE; e < n * n; e += WAVE) {
     const int i = e / n, j = e - n * (e / n);
     if (i < m && j < m) {
@@ -4533,18 +4542,18 @@ __device__ __forceinline__ bool newton_treeblk(const Model<float>& M, const Ws<f
     grest[i] = i < m ? g[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] : g[0] + (double)LY;
   SYNC();
   if (M.dbg_flags & 8192)
-    chol_solve_reg<float, TB_MAXR>(R, w.bc(), n, grest, xr);
+    chol_solve_reg<T, TB_MAXR>(R, w.bc(), n, grest, xr);
   else
-    chol_solve_rl<TB_MAXR>(R, n, grest, xr);
+    chol_solve_rl<TB_MAXR, T>(R, n, grest, xr);
   // ---- back substitution: the coupled positions and the belt from the dense solve, the singles on their lanes
-  const float xb = xr[m];
+  const T xb = xr[m];
   for (int i = LANE; i < m; i += WAVE) dir[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] = xr[i];
   if (LANE == 0) dir[0] = xb;
   if (single) {
-    float x[9];
+    T x[9];
 #pragma unroll
     for (int i = 8; i >= 0; i--) {
-      float a = y[i] - lb[i] * xb;
+      T a = y[i] - lb[i] * xb;
 #pragma unroll
       for (int k = i + 1; k < 9; k++) a -= Lb[P9(k, i)] * x[k];
       x[i] = a * dv[i];
@@ -4666,7 +4675,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       }
     }
     if constexpr (treeblk_scene<T, DIM>()) {
-      if (!solved && !(M.dbg_flags & (2048 | 3)) && newton_treeblk<DIM>(M, w, g, dir, ncon, nrow)) {
+      if (!solved && !(M.dbg_flags & (2048 | 3)) && newton_treeblk<T, DIM>(M, w, g, dir, ncon, nrow)) {
         PMARK(PH_NCHOL);
         solved = true;
       }

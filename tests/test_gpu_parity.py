@@ -375,9 +375,10 @@ def test_config5_kernel_is_deterministic():
 @pytest.mark.parametrize("env_class", ["PauseIKToggleEnv", "BackupIKToggleEnv"])
 def test_teacher_forced_ik_classes_fp64_4x16(oracle, env_class):
     """BASELINE config 5's scene (4 arms x 16 cubes, environments.py:580-645, ik_policy.py:141-282) in the
-    parity-grade fp64 build: the arena exceeds the CU's 160 KiB of LDS in float64, so the Newton Hessian and the
-    contact records run from a per-arena global scratch block (DimsSpill, fm_dev.hpp).  150 teacher-forced
-    env-steps: IK FSM block and every integer exact, IK doubles within 1e-6, state within 1e-5"""
+    parity-grade fp64 build: since round 5 the compile-time FixedDims<4, 16> fp64 kernel (Hessian and contact records
+    in the arena's global scratch block, the tree-block Newton solve in float64) -- the runtime DimsSpill kernel no
+    longer runs it.  150 teacher-forced env-steps: IK FSM block and every integer exact, IK doubles within 1e-6, state
+    within 1e-5"""
     traj = pu.rollout(oracle, 4, 16, 150, seed_actions=13, env_class=env_class)
     r = pu.compare(traj, "fp64", 4, 16, env_class, verbose_tol=1e-6)
     print(f"fp64 (4,16) {env_class}: worst rel err {r['errs'].max():.3e}, obs {r['obs_err'].max():.2e}, "
