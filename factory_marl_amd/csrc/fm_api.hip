@@ -106,6 +106,7 @@ struct fm_handle {
   // the IK classes' record backup, the wide kernel's layout
   int32_t* rerun = nullptr;
   char* bak = nullptr;
+  double* resume = nullptr;    // [N][resume_stride] substep state of an abandoned env-step
   Lay lay_rerun{};
   char* spill_buf = nullptr;   // [N][spill_stride]
   bool ktime_on = false;                                   // fm_kernel_timing
@@ -207,7 +208,7 @@ static Model<T> make_model(const fm_handle* h) {
 // experiment switches of the kernel (A/B probes and the equivalence tests; every default is 0): read from the
 // environment once, at fm_create, and reported on stderr when any is set; "experiment_flags" (fm_set_param) changes
 // them on a live handle for later launches
-constexpr uint32_t FM_XFLAGS_MASK = 0x3FFFu;  // the switches below (fm_set_param rejects other bits)
+constexpr uint32_t FM_XFLAGS_MASK = 0x7FFFu;  // the switches below (fm_set_param rejects other bits)
 static uint32_t read_experiment_flags() {
   struct Sw {
     const char* var;
@@ -229,6 +230,7 @@ static uint32_t read_experiment_flags() {
       {"FM_NO_TREEBLK", '1', 2048},    // (2,8), (2,10), (4,16) fp32, wide rerun: the dense Hessian + factors on every substep
       {"FM_PC_SCATTER", '1', 4096},    // (2,4): J' f by the per-contact scatter instead of per (contact, column)
       {"FM_TB_LDSBC", '1', 8192},      // tree-block solve: its coupled system by the LDS-broadcast register factor
+      {"FM_RERUN_AT_50", '1', 16384},  // (2,4): every env-step abandoned at substep 50, resumed there by the wide kernel
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {
@@ -466,6 +468,10 @@ static int create_typed(fm_handle* h) {
     HIPCHK(hipMalloc((void**)&h->rerun, (N + 1) * sizeof(int32_t)));
     h->allocs.push_back(h->rerun);
     HIPCHK(hipMemset(h->rerun, 0, (N + 1) * sizeof(int32_t)));
+    // the substep state of an abandoned env-step (the wide kernel resumes from it, fm_dev.hpp State::resume)
+    HIPCHK(hipMalloc((void**)&h->resume, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
+    h->allocs.push_back(h->resume);
+    HIPCHK(hipMemset(h->resume, 0, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
     if (h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS) {
       HIPCHK(hipMalloc((void**)&h->bak, N * (8 * (size_t)d.dbl_stride + 4 * (size_t)d.int_stride)));
       h->allocs.push_back(h->bak);
@@ -583,6 +589,7 @@ static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik) {
   pr.S.order = nullptr;
   pr.S.rerun = h->rerun;
   pr.S.bak = h->bak;
+  pr.S.resume = h->resume;
   pr.M.dm.maxcon = MAXCON_WIDE;  // the wide kernel keeps up to 128 contacts per stage
   rerun_launch<T, 2, 4>(pr, h->dm.N, h->stream, ik);
 }
@@ -629,6 +636,7 @@ static void launch_step(fm_handle* h, const StepIO& io) {
       pf.M.ovf_abort = 1;                                                                              \
       pf.S.rerun = h->rerun;                                                                           \
       pf.S.bak = h->bak;                                                                               \
+      pf.S.resume = h->resume;                                                                         \
     }                                                                                                  \
     ktime_begin(h);                                                                                    \
     fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream, ik);                              \
@@ -880,7 +888,7 @@ int fm_set_param(fm_handle* h, const char* name, double value) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   if (name && std::string(name) == "experiment_flags") {
     if (!(value >= 0 && value < 65536 && value == (double)(uint32_t)value) || ((uint32_t)value & ~FM_XFLAGS_MASK))
-      return set_err(FM_EINVAL, "bad flags: experiment switches are the bits of 0x3FFF (fm_api.hip read_experiment_flags)");
+      return set_err(FM_EINVAL, "bad flags: experiment switches are the bits of 0x7FFF (fm_api.hip read_experiment_flags)");
     h->xflags = (uint32_t)value;
     return FM_OK;
   }

@@ -163,7 +163,14 @@ struct State {
   // IK classes with `rerun`: the arena's task records (dbl, ints) as the env-step found them, restored by the rerun
   // (the IK compose writes the FSM and the toggles' last actions before the substeps)
   gptr<char> bak{nullptr};
+  // with `rerun`: per arena the substep state at which the 64-contact kernel abandoned its env-step (resume_stride
+  // doubles: [0] substep t, [1] [2] the contact counters of the stages so far, qpos nq, qvel nv, qacc warmstart nv,
+  // ctrl nu, clipped control target nu), so the wide kernel resumes at substep t instead of redoing the env-step;
+  // t = 0: nothing done yet, the wide kernel runs the whole env-step
+  gptr<double> resume{nullptr};
 };
+// doubles per arena of State::resume
+__host__ __device__ constexpr int resume_stride(int nq, int nv, int nu) { return 3 + nq + 2 * nv + 2 * nu; }
 
 // the arena's global scratch block (nullptr unless the kernel runs a DimsSpill layout)
 template <typename DIM, typename T>

@@ -5702,11 +5702,18 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
 #define rng (S.rng + 4 * (size_t)ARENA_)
 #define ctr (S.counters + FM_NCTR * (size_t)ARENA_)
 #define act (io.actions + (size_t)ARENA_ * dm.act_dim)
+  // the wide rerun kernel resumes an env-step the 64-contact kernel abandoned after substep 0 (State::resume): the
+  // IK compose, the clipped control target and substeps 0 .. t0-1 are already done (their task-record writes stand)
+  int t0 = 0;
+  if constexpr (DIM::rerun) {
+    const double* const rs = S.resume;
+    if (rs) t0 = (int)rs[(size_t)ARENA_ * resume_stride(dm.nq, dm.nv, nu)];
+  }
   if constexpr (IK && (can_abandon || DIM::rerun)) {
     // the IK compose below writes the FSM / last-action blocks of the task records: keep the step's starting
     // records for a rerun (the rerun restores them first)
     char* const bk = S.bak;
-    if (bk) {
+    if (bk && t0 == 0) {
       double* bd = (double*)(bk + (size_t)arena * (8 * dm.dbl_stride + 4 * dm.int_stride));
       int32_t* bi = (int32_t*)(bd + dm.dbl_stride);
       double* dd = S.dbl + (size_t)arena * dm.dbl_stride;
@@ -5735,6 +5742,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
   const double speed0 = td[1];
   const int ec = M.env_class;
   double* prop = (double*)w.H() + 24 * A;  // IK proposals of this step's compose (phase-local scratch)
+  if (t0 == 0) {
   if (IK && env_ik_at_step(ec)) {  // IKPolicy.act() on the state the step starts from
     load_state(M, S, w, arena, false);
     SYNC();
@@ -5789,6 +5797,30 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
   // stage (mj_step1) at the state of the last mj_step1 (pre-teleport), then integrate the current state
   load_state(M, S, w, arena, true);
   SYNC();
+  } else if constexpr (DIM::rerun) {
+    // resume: the substep state the 64-contact kernel saved when its stage t0 exceeded 64 contacts
+    const double* r = (const double*)S.resume + (size_t)ARENA_ * resume_stride(dm.nq, dm.nv, nu);
+    if (LANE == 0) {
+      w.misc()[MISC_CSUM] = (int)r[1];
+      w.misc()[MISC_CMAX] = (int)r[2];
+    }
+    r += 3;
+    for (int i = LANE; i < dm.nq; i += WAVE) w.qd()[i] = r[i];
+    r += dm.nq;
+    for (int i = LANE; i < dm.nv; i += WAVE) {
+      w.vd()[i] = r[i];
+      w.a()[i] = r[dm.nv + i];
+    }
+    r += 2 * dm.nv;
+    for (int u = LANE; u < nu; u += WAVE) {
+      ctrl_[u] = r[u];
+      uctl_[u] = r[nu + u];
+    }
+    init_arena(M, w, arena);
+    SYNC();
+    refresh_copies(M, w);
+    SYNC();
+  }
 #define lp (0.001 / (0.001 + M.pt_time))
 #define phw (S.phys + (size_t)ARENA_ * dm.phys_stride)
 #define sc_ (w.scal())  // [0] reward, [1] terminated, [2] out_of_reach, [3] force_terminate
@@ -5797,12 +5829,35 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
   // substep walks through small enough for the instruction cache:
   //   t = 0..frame_skip-1:  mj_step1 (stage) ; ctrl low-pass ; mj_step2 (smooth acc, solve, integrate)
   //   then the task layer; on termination one more pass = reset_sim's forward (stage, smooth, solve).
-  for (int t = 0;; t++) {
+  for (int t = t0;; t++) {
     stage(M, w, arena, ctr);
     if constexpr (can_abandon) {
       // uniform (LDS scalar); experiment switch 512 (FM_FORCE_RERUN=1): every env-step goes to the wide kernel
-      if (S.rerun && (w.misc()[MISC_OVF] > 0 || (M.dbg_flags & 512))) {
+      // switch 16384 (FM_RERUN_AT_50=1): every env-step abandoned at substep 50 (the resume path's parity test)
+      if (S.rerun && (w.misc()[MISC_OVF] > 0 || (M.dbg_flags & 512) || ((M.dbg_flags & 16384) && t == 50))) {
         if (!reset_pass) {
+          double* const rs = S.resume;
+          if (rs) {
+            // the substep state for the wide kernel to resume from (substeps 0 .. t-1 done; stage t is redone there)
+            double* r = rs + (size_t)ARENA_ * resume_stride(dm.nq, dm.nv, nu);
+            if (LANE == 0) {
+              r[0] = (double)t;
+              r[1] = (double)w.misc()[MISC_CSUM];
+              r[2] = (double)w.misc()[MISC_CMAX];
+            }
+            r += 3;
+            for (int i = LANE; i < dm.nq; i += WAVE) r[i] = w.qd()[i];
+            r += dm.nq;
+            for (int i = LANE; i < dm.nv; i += WAVE) {
+              r[i] = w.vd()[i];
+              r[dm.nv + i] = w.a()[i];
+            }
+            r += 2 * dm.nv;
+            for (int u = LANE; u < nu; u += WAVE) {
+              r[u] = ctrl_[u];
+              r[nu + u] = uctl_[u];
+            }
+          }
           if (LANE == 0) {
             int32_t* const rr = S.rerun;
             rr[1 + atomicAdd(rr, 1)] = arena;
