@@ -440,11 +440,13 @@ def make_roofline(args, N, A, K, kern_ms, traffic_json, valu_json):
             "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
             "kernel": "fm::step_kernel", "kernel_ms_avg": round(kern_ms, 4),
             "algorithmic_bytes_per_arena_step": B,
-            "binding": "neither HBM nor MFMA: dependent LDS / VALU / L2 latency chains, two waves (arenas) per SIMD"}
+            "binding": "neither HBM nor MFMA: dependent LDS / VALU (fp32 + fp64) / L2 latency chains, one arena per "
+                       "wave, two waves per SIMD (config 2)"}
     if traffic is not None:
-        roof["traffic_note"] = ("PMC TCC -> memory-fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE): the per-arena "
-                                "scratch blocks (contact records, Hessian) and register spills that leave the L2, "
-                                "whether the MALL or HBM serves them; %.1f %% of the HBM peak at this launch time"
+        roof["traffic_note"] = ("PMC TCC -> memory-fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, "
+                                + os.path.relpath(traffic_json, ROOT) + "): the per-arena scratch blocks (contact "
+                                "records, Hessian) written back when the L2 evicts them, whether the MALL or HBM takes "
+                                "them (no register spills since round 5); %.2f %% of the HBM peak at this launch time"
                                 % (100.0 * traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS))
     vj = load_json(valu_json) or {}
     if vj.get("A") == A and vj.get("K") == K and vj.get("precision") == args.precision:

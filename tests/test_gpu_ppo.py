@@ -66,3 +66,43 @@ def test_reference_policy_drives_gpu_env(run):
           f"contacts dropped {int(cnt[:, 0].sum())}, max contacts {int(cnt[:, 5].max())}")
     assert torch.isfinite(obs).all() and torch.isfinite(ret).all()
     env.close()
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+def test_rccl_collectives_execute_on_the_gpu():
+    """the trainer's RCCL path on hardware (backend "nccl" = RCCL on ROCm), one rank on the box's one GPU: the process
+    group opened as launch.RankContext opens it for GPU ranks, a device all-reduce, and one PPO iteration with the
+    group live -- initial-weight broadcast, the asynchronous advantage-statistics all-reduce and the fused gradient
+    all-reduce (ppo.py) all go through RCCL kernels.  (The 8-GPU node is the driver's; world 1 exercises the calls.)"""
+    import socket
+
+    import torch.distributed as dist
+
+    from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.environments import run_kwargs
+    from factory_marl_amd.launch import reduce_over_ranks
+    from factory_marl_amd.ppo import PPO
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        t = torch.arange(16, dtype=torch.float32, device=dev)
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, torch.arange(16, dtype=torch.float32, device=dev))
+        assert reduce_over_ranks(2.5, "max", dev) == 2.5
+        env = FactoryVecEnv(256, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=2, max_num_objects=4,
+                                                        seed=42))
+        ppo = PPO(env, n_steps=4, batch_size=512, n_epochs=1, seed=0, dist=dist)
+        assert ppo.dist is not None and ppo.world == 1
+        ppo.learn(256 * 4)
+        rec = ppo.logs[-1]
+        assert all(np.isfinite(rec[k]) for k in ["policy_loss", "value_loss", "entropy_loss"])
+        env.close()
+    finally:
+        dist.destroy_process_group()
