@@ -34,6 +34,29 @@ void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStre
 // =================================================================================================
 using namespace fm;
 
+// the CPU backend's kernels (fm_cpu.cpp: fm_device.hpp compiled for the host, the wave emulated)
+extern "C" void fm_cpu_step(int fp64, const void* params, int num_arenas, int lds_bytes, int ik);
+extern "C" void fm_cpu_reset(int fp64, const void* model, const void* state, const void* lay, float* obs,
+                             const uint8_t* mask, int num_arenas, int lds_bytes);
+extern "C" void fm_cpu_debug(int fp64, const void* model, const void* state, const void* lay, int arena, int actuated,
+                             double* out, int lds_bytes);
+namespace fm {
+template <typename T>
+static void cpu_step(const StepParams<T>& p, int num_arenas, int lds_bytes, bool ik) {
+  fm_cpu_step(sizeof(T) == 8, &p, num_arenas, lds_bytes, ik ? 1 : 0);
+}
+template <typename T>
+static void cpu_reset(const Model<T>& M, const State<T>& S, const Lay& L, float* obs, const uint8_t* mask,
+                      int num_arenas, int lds_bytes) {
+  fm_cpu_reset(sizeof(T) == 8, &M, &S, &L, obs, mask, num_arenas, lds_bytes);
+}
+template <typename T>
+static void cpu_debug(const Model<T>& M, const State<T>& S, const Lay& L, int arena, int actuated, double* out,
+                      int lds_bytes) {
+  fm_cpu_debug(sizeof(T) == 8, &M, &S, &L, arena, actuated, out, lds_bytes);
+}
+}  // namespace fm
+
 static thread_local std::string g_err;
 
 static int set_err(int code, const std::string& msg) {
@@ -56,6 +79,7 @@ struct fm_handle {
   hipStream_t own_stream = nullptr;  // the private stream fm_create made; the only one fm_destroy destroys
   hipEvent_t handoff = nullptr;      // orders a new stream after the work queued on the previous one
   bool fp64 = false;
+  bool cpu = false;  // device = -1: the CPU backend (fm_cpu.cpp), every array in host memory
   bool was_reset = false;
   Lay lay;
   std::vector<void*> allocs;
@@ -114,28 +138,62 @@ struct fm_handle {
   long long spill_stride = 0;  // Lay::gtotal of the spill layout in use (compile-time scenes; runtime fp64 (4,16))
 };
 
+// memory of the handle's arrays: device memory, or host memory for the CPU backend (device = -1)
+template <typename P>
+static hipError_t d_malloc(fm_handle* h, P** p, size_t n) {
+  if (h->cpu) {
+    *p = (P*)std::calloc(n ? n : 1, 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+  }
+  return hipMalloc((void**)p, n);
+}
+static hipError_t d_free(fm_handle* h, void* p) {
+  if (h->cpu) {
+    std::free(p);
+    return hipSuccess;
+  }
+  return hipFree(p);
+}
+static hipError_t d_memcpy(fm_handle* h, void* dst, const void* src, size_t n, hipMemcpyKind k) {
+  if (h->cpu) {
+    if (n) std::memcpy(dst, src, n);
+    return hipSuccess;
+  }
+  return hipMemcpy(dst, src, n, k);
+}
+static hipError_t d_memset(fm_handle* h, void* p, int v, size_t n) {
+  if (h->cpu) {
+    std::memset(p, v, n);
+    return hipSuccess;
+  }
+  return hipMemset(p, v, n);
+}
+static hipError_t d_setdev(fm_handle* h) { return h->cpu ? hipSuccess : hipSetDevice(h->device); }
+static hipError_t d_sync(fm_handle* h) { return h->cpu ? hipSuccess : hipStreamSynchronize(h->stream); }
+
 template <typename T>
 static int upload(fm_handle* h, void** dst, const std::vector<double>& src) {
   std::vector<T> tmp(src.size());
   for (size_t i = 0; i < src.size(); i++) tmp[i] = (T)src[i];
   size_t bytes = std::max<size_t>(tmp.size(), 1) * sizeof(T);
-  HIPCHK(hipMalloc(dst, bytes));
+  HIPCHK(d_malloc(h, dst, bytes));
   h->allocs.push_back(*dst);
-  if (!tmp.empty()) HIPCHK(hipMemcpy(*dst, tmp.data(), tmp.size() * sizeof(T), hipMemcpyHostToDevice));
+  if (!tmp.empty()) HIPCHK(d_memcpy(h, *dst, tmp.data(), tmp.size() * sizeof(T), hipMemcpyHostToDevice));
   return 0;
 }
 
 template <typename U>
 static int upload_raw(fm_handle* h, U** dst, const std::vector<U>& src) {
   size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(U);
-  HIPCHK(hipMalloc((void**)dst, bytes));
+  HIPCHK(d_malloc(h, (void**)dst, bytes));
   h->allocs.push_back(*dst);
-  if (!src.empty()) HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(U), hipMemcpyHostToDevice));
+  if (!src.empty()) HIPCHK(d_memcpy(h, *dst, src.data(), src.size() * sizeof(U), hipMemcpyHostToDevice));
   return 0;
 }
 
 static Lay lds_layout(const Dims& d, int tsize, bool spill = false) {
-  return make_layout(d.A, d.K, d.nq, d.nv, d.nu, d.ngc, d.ncb, d.maxcon, d.maxrow, d.ntree, tsize, spill);
+  return make_layout(d.A, d.K, d.nq, d.nv, d.nu, d.ngc, d.ncb, d.maxcon, d.maxrow, d.ntree, tsize, spill, false, false,
+                     false, false, false, Dims::MAXC / WAVE);
 }
 
 template <typename T>
@@ -373,12 +431,12 @@ static int create_typed(fm_handle* h) {
   // state
   size_t N = d.N;
   // the physics state is float64 in both precisions (fp32 computes from float copies of it)
-  HIPCHK(hipMalloc(&h->phys, N * d.phys_stride * sizeof(double)));
+  HIPCHK(d_malloc(h, &h->phys, N * d.phys_stride * sizeof(double)));
   h->allocs.push_back(h->phys);
-  HIPCHK(hipMemset(h->phys, 0, N * d.phys_stride * sizeof(double)));
-  HIPCHK(hipMalloc((void**)&h->dbl, N * d.dbl_stride * sizeof(double)));
+  HIPCHK(d_memset(h, h->phys, 0, N * d.phys_stride * sizeof(double)));
+  HIPCHK(d_malloc(h, (void**)&h->dbl, N * d.dbl_stride * sizeof(double)));
   h->allocs.push_back(h->dbl);
-  HIPCHK(hipMalloc((void**)&h->ints, N * d.int_stride * sizeof(int32_t)));
+  HIPCHK(d_malloc(h, (void**)&h->ints, N * d.int_stride * sizeof(int32_t)));
   h->allocs.push_back(h->ints);
   {
     // IKPolicy.__init__ (ik_policy.py:76-81) + PauseIKToggleEnv.last_arm_actions (environments.py:592): idle,
@@ -393,21 +451,28 @@ static int create_typed(fm_handle* h) {
         ii[2] = -1;
         for (int o = 0; o < d.A; o++) ii[3 + o] = -1;
       }
-    HIPCHK(hipMemcpy(h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(d_memcpy(h, h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(d_memcpy(h, h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
   if ((r = upload_raw<uint64_t>(h, &h->rng, s.rng_init))) return r;
-  HIPCHK(hipMalloc((void**)&h->counters, N * FM_NCTR * sizeof(int64_t)));
+  HIPCHK(d_malloc(h, (void**)&h->counters, N * FM_NCTR * sizeof(int64_t)));
   h->allocs.push_back(h->counters);
-  HIPCHK(hipMemset(h->counters, 0, N * FM_NCTR * sizeof(int64_t)));
-  if (!getenv("FACTORYSIM_NO_LPT")) {  // experiment switch: plain blockIdx -> arena dispatch
-    HIPCHK(hipMalloc((void**)&h->cost, N * sizeof(uint32_t)));
+  HIPCHK(d_memset(h, h->counters, 0, N * FM_NCTR * sizeof(int64_t)));
+  if (!getenv("FACTORYSIM_NO_LPT") && !h->cpu) {  // experiment switch: plain blockIdx -> arena dispatch
+    HIPCHK(d_malloc(h, (void**)&h->cost, N * sizeof(uint32_t)));
     h->allocs.push_back(h->cost);
-    HIPCHK(hipMemset(h->cost, 0, N * sizeof(uint32_t)));
-    HIPCHK(hipMalloc((void**)&h->order, N * sizeof(int32_t)));
+    HIPCHK(d_memset(h, h->cost, 0, N * sizeof(uint32_t)));
+    HIPCHK(d_malloc(h, (void**)&h->order, N * sizeof(int32_t)));
     h->allocs.push_back(h->order);
   }
   h->lay = lds_layout(d, sizeof(T));
+  if (h->cpu) {
+    // CPU backend: the runtime-dims kernel with its whole workspace in the emulated wave's host "LDS" (no 160 KiB
+    // limit, no spill layout, no compile-time scenes, no dispatch order)
+    h->lay_step = h->lay;
+    h->fixed = -1;
+    return 0;
+  }
   if (h->lay.total > 160 * 1024) {
     if constexpr (sizeof(T) == 8) {
       // fp64 scenes beyond the CU's LDS (4 arms): the parity-grade spill layout (DimsSpill, fm_dev.hpp)
@@ -415,7 +480,7 @@ static int create_typed(fm_handle* h) {
       if (h->lay.total > 160 * 1024) return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
       h->spill = true;
       h->spill_stride = h->lay.gtotal;
-      HIPCHK(hipMalloc((void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay.gtotal));
+      HIPCHK(d_malloc(h, (void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay.gtotal));
       h->allocs.push_back(h->spill_buf);
       HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, DimsSpill>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  h->lay.total));
@@ -458,22 +523,22 @@ static int create_typed(fm_handle* h) {
   (void)idx;
   if (h->fixed >= 0 && h->lay_step.spill) {  // compile-time scenes: the Hessian + contact records in global scratch
     h->spill_stride = h->lay_step.gtotal;
-    HIPCHK(hipMalloc((void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay_step.gtotal));
+    HIPCHK(d_malloc(h, (void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay_step.gtotal));
     h->allocs.push_back(h->spill_buf);
   }
   // the benchmark scene at its 64-contact capacity: an env-step with a stage above it is rerun by the wide kernel
   if (h->fixed >= 0 && FixedDims<2, 4>::matches(d) && d.maxcon == MAXCON) {
     HIPCHK((rerun_set_attr<T, 2, 4>()));
     h->lay_rerun = rerun_layout<T, 2, 4>();
-    HIPCHK(hipMalloc((void**)&h->rerun, (N + 1) * sizeof(int32_t)));
+    HIPCHK(d_malloc(h, (void**)&h->rerun, (N + 1) * sizeof(int32_t)));
     h->allocs.push_back(h->rerun);
-    HIPCHK(hipMemset(h->rerun, 0, (N + 1) * sizeof(int32_t)));
+    HIPCHK(d_memset(h, h->rerun, 0, (N + 1) * sizeof(int32_t)));
     // the substep state of an abandoned env-step (the wide kernel resumes from it, fm_dev.hpp State::resume)
-    HIPCHK(hipMalloc((void**)&h->resume, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
+    HIPCHK(d_malloc(h, (void**)&h->resume, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
     h->allocs.push_back(h->resume);
-    HIPCHK(hipMemset(h->resume, 0, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
+    HIPCHK(d_memset(h, h->resume, 0, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
     if (h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS) {
-      HIPCHK(hipMalloc((void**)&h->bak, N * (8 * (size_t)d.dbl_stride + 4 * (size_t)d.int_stride)));
+      HIPCHK(d_malloc(h, (void**)&h->bak, N * (8 * (size_t)d.dbl_stride + 4 * (size_t)d.int_stride)));
       h->allocs.push_back(h->bak);
     }
   }
@@ -500,11 +565,11 @@ static int get_state_typed(fm_handle* h, char* out) {
   std::vector<double> db(N * d.dbl_stride);
   std::vector<int32_t> in(N * d.int_stride);
   std::vector<uint64_t> rg(N * 4);
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(ph.data(), h->phys, ph.size() * sizeof(double), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(db.data(), h->dbl, db.size() * sizeof(double), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(in.data(), h->ints, in.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(rg.data(), h->rng, rg.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(d_sync(h));
+  HIPCHK(d_memcpy(h, ph.data(), h->phys, ph.size() * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(d_memcpy(h, db.data(), h->dbl, db.size() * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(d_memcpy(h, in.data(), h->ints, in.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(d_memcpy(h, rg.data(), h->rng, rg.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   size_t rec = state_record_size(h);
   for (size_t n = 0; n < N; n++) {
     char* o = out + n * rec;
@@ -539,11 +604,11 @@ static int set_state_typed(fm_handle* h, const char* src) {
         (const uint64_t*)(o + (d.phys_stride + d.dbl_stride) * sizeof(double) + d.int_stride * sizeof(int32_t));
     for (int i = 0; i < 4; i++) rg[n * 4 + i] = up[i];
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(h->phys, ph.data(), ph.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->rng, rg.data(), rg.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  HIPCHK(d_sync(h));
+  HIPCHK(d_memcpy(h, h->phys, ph.data(), ph.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(d_memcpy(h, h->dbl, db.data(), db.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(d_memcpy(h, h->ints, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(d_memcpy(h, h->rng, rg.data(), rg.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   h->was_reset = true;
   return FM_OK;
 }
@@ -616,6 +681,11 @@ static void ktime_clear(fm_handle* h) {
 
 template <typename T>
 static void launch_step(fm_handle* h, const StepIO& io) {
+  if (h->cpu) {
+    const StepParams<T> pc{make_model<T>(h), make_state<T>(h), h->lay, io};
+    cpu_step<T>(pc, h->dm.N, h->lay.total, h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS);
+    return;
+  }
   if (h->order) hipLaunchKernelGGL(lpt_order_kernel, dim3(1), dim3(1024), 0, h->stream, h->cost, h->order, h->dm.N);
   bool rerun = h->rerun && !(h->xflags & 1024);
   if (rerun && hipMemsetAsync(h->rerun, 0, sizeof(int32_t), h->stream) != hipSuccess) {
@@ -808,18 +878,24 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
   d.phys_stride = 2 * s.nq + 3 * s.nv;
   d.dbl_stride = s.nu + 3 + 2 * s.A + 1 + 27 * s.A;
   d.int_stride = 2 * s.K + I_NINT + (3 + s.A) * s.A;
-  if (hipSetDevice(device) != hipSuccess) {
-    delete h;
-    return set_err(FM_EDEVICE, "hipSetDevice failed");
-  }
-  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
-    return set_err(FM_EDEVICE, "hipStreamCreate failed");
-  }
-  h->stream = h->own_stream;
-  if (hipEventCreateWithFlags(&h->handoff, hipEventDisableTiming) != hipSuccess) {
-    fm_destroy(h);
-    return set_err(FM_EDEVICE, "hipEventCreate failed");
+  if (device < 0) {
+    // device = -1: the CPU backend (BASELINE config 1, one env on the host): host arrays, the kernels
+    // of fm_device.hpp run on host threads with the wave emulated (fm_cpu.cpp); every pointer argument is host memory
+    h->cpu = true;
+  } else {
+    if (hipSetDevice(device) != hipSuccess) {
+      delete h;
+      return set_err(FM_EDEVICE, "hipSetDevice failed (no GPU?  device = -1 selects the CPU backend)");
+    }
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+      delete h;
+      return set_err(FM_EDEVICE, "hipStreamCreate failed");
+    }
+    h->stream = h->own_stream;
+    if (hipEventCreateWithFlags(&h->handoff, hipEventDisableTiming) != hipSuccess) {
+      fm_destroy(h);
+      return set_err(FM_EDEVICE, "hipEventCreate failed");
+    }
   }
   int r = h->fp64 ? create_typed<double>(h) : create_typed<float>(h);
   if (r) {
@@ -833,12 +909,17 @@ int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle
 
 void fm_destroy(fm_handle* h) {
   if (!h) return;
-  (void)hipSetDevice(h->device);
+  if (h->cpu) {
+    for (void* p : h->allocs) std::free(p);
+    delete h;
+    return;
+  }
+  (void)d_setdev(h);
   // the arena state may still be in use by work queued on the current stream (the caller's or ours)
-  (void)hipStreamSynchronize(h->stream);
+  (void)d_sync(h);
   if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
   ktime_clear(h);
-  for (void* p : h->allocs) (void)hipFree(p);
+  for (void* p : h->allocs) (void)d_free(h, p);
   for (void* p : {(void*)h->render_rgb, (void*)h->cube_rgba, (void*)h->render_frames, (void*)h->render_arenas})
     if (p) (void)hipFree(p);
   if (h->render_arenas_host) (void)hipHostFree(h->render_arenas_host);
@@ -850,11 +931,12 @@ void fm_destroy(fm_handle* h) {
 
 int fm_set_stream(fm_handle* h, void* stream) {
   if (!h) return set_err(FM_EINVAL, "null handle");
+  if (h->cpu) return FM_OK;  // the CPU backend runs synchronously in the calling thread's launches
   hipStream_t next = (hipStream_t)stream;  // NULL = the legacy default stream (torch's default stream)
   if (next == h->stream) return FM_OK;
   // arena state is shared by every call of the handle: work queued on the new stream must not start
   // before what is already queued on the old one (a step on stream B racing a step on stream A)
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
   HIPCHK(hipEventRecord(h->handoff, h->stream));
   HIPCHK(hipStreamWaitEvent(next, h->handoff, 0));
   h->stream = next;
@@ -917,9 +999,9 @@ int fm_num_counters(void) { return FM_NCTR; }
 
 int fm_sync(fm_handle* h) {
   if (!h) return set_err(FM_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipGetLastError());
+  HIPCHK(d_setdev(h));
+  HIPCHK(d_sync(h));
+  if (!h->cpu) HIPCHK(hipGetLastError());
   return FM_OK;
 }
 
@@ -934,7 +1016,15 @@ int fm_workspace_bytes(const fm_handle* h) { return h ? h->lay_step.total : -1; 
 int fm_reset(fm_handle* h, const uint8_t* mask, void* obs_) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   float* obs = (float*)obs_;  // float64 rows when cfg.obs_float64 (Model::obs64): the kernel writes the row type
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
+  if (h->cpu) {
+    if (h->fp64)
+      cpu_reset<double>(make_model<double>(h), make_state<double>(h), h->lay, obs, mask, h->dm.N, h->lay.total);
+    else
+      cpu_reset<float>(make_model<float>(h), make_state<float>(h), h->lay, obs, mask, h->dm.N, h->lay.total);
+    h->was_reset = true;
+    return FM_OK;
+  }
   dim3 grid(h->dm.N), block(WAVE);
   if (h->fp64 && h->spill) {
     hipLaunchKernelGGL((reset_kernel<double, DimsSpill>), grid, block, h->lay.total, h->stream, make_model<double>(h),
@@ -956,7 +1046,7 @@ int fm_step(fm_handle* h, const float* actions, void* obs, float* reward, uint8_
   if (!h) return set_err(FM_EINVAL, "null handle");
   if (!actions && h->dm.act_dim > 0) return set_err(FM_EINVAL, "actions is NULL");
   if (!h->was_reset) return set_err(FM_ESTATE, "fm_step before fm_reset");
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
   StepIO io;
   std::memset(&io, 0, sizeof io);
   io.actions = actions;
@@ -980,7 +1070,7 @@ int fm_step(fm_handle* h, const float* actions, void* obs, float* reward, uint8_
     launch_step<double>(h, io);
   else
     launch_step<float>(h, io);
-  HIPCHK(hipGetLastError());
+  if (!h->cpu) HIPCHK(hipGetLastError());
   return FM_OK;
 }
 
@@ -989,13 +1079,13 @@ int fm_state_size(const fm_handle* h) { return h ? state_record_size(h) : -1; }
 
 int fm_get_state(fm_handle* h, void* host_out) {
   if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
   return h->fp64 ? get_state_typed<double>(h, (char*)host_out) : get_state_typed<float>(h, (char*)host_out);
 }
 
 int fm_set_state(fm_handle* h, const void* host_in) {
   if (!h || !host_in) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
   return h->fp64 ? set_state_typed<double>(h, (const char*)host_in) : set_state_typed<float>(h, (const char*)host_in);
 }
 
@@ -1004,10 +1094,19 @@ int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int c
   const Dims& d = h->dm;
   int need = 2 + 81 * d.A + 4 * d.nv + 3 * d.A + 60 * d.A + 27 * d.A + 17 * 64 + 6 * 20 * d.A;
   if (cap < need) return set_err(FM_EINVAL, "buffer too small: need " + std::to_string(need));
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
   double* dbuf = nullptr;
-  HIPCHK(hipMalloc(&dbuf, need * sizeof(double)));
-  HIPCHK(hipMemset(dbuf, 0, need * sizeof(double)));
+  HIPCHK(d_malloc(h, &dbuf, need * sizeof(double)));
+  HIPCHK(d_memset(h, dbuf, 0, need * sizeof(double)));
+  if (h->cpu) {
+    if (h->fp64)
+      cpu_debug<double>(make_model<double>(h), make_state<double>(h), h->lay, arena, actuated, dbuf, h->lay.total);
+    else
+      cpu_debug<float>(make_model<float>(h), make_state<float>(h), h->lay, arena, actuated, dbuf, h->lay.total);
+    std::memcpy(host_out, dbuf, need * sizeof(double));
+    std::free(dbuf);
+    return need;
+  }
   if (h->fp64 && h->spill) {
     HIPCHK(hipFuncSetAttribute((const void*)debug_kernel<double, DimsSpill>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, h->lay.total));
@@ -1025,30 +1124,31 @@ int fm_debug_dump(fm_handle* h, int arena, int actuated, double* host_out, int c
                        make_state<float>(h), h->lay, arena, actuated, dbuf);
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(host_out, dbuf, need * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(d_sync(h));
+  HIPCHK(d_memcpy(h, host_out, dbuf, need * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(dbuf));
   return need;
 }
 
 int fm_profile(fm_handle* h, int mode, uint64_t* host_out) {
   if (!h) return set_err(FM_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(h->device));
+  if (h->cpu) return set_err(FM_EINVAL, "the phase profile is GPU-only (wall-clock ticks of the device)");
+  HIPCHK(d_setdev(h));
   if (!h->prof) {
-    HIPCHK(hipMalloc((void**)&h->prof, FM_NPROF * sizeof(unsigned long long)));
+    HIPCHK(d_malloc(h, (void**)&h->prof, FM_NPROF * sizeof(unsigned long long)));
     h->allocs.push_back(h->prof);
-    HIPCHK(hipMemset(h->prof, 0, FM_NPROF * sizeof(unsigned long long)));
+    HIPCHK(d_memset(h, h->prof, 0, FM_NPROF * sizeof(unsigned long long)));
   }
   if (host_out) {
-    HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemcpy(host_out, h->prof, FM_NPROF * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(d_sync(h));
+    HIPCHK(d_memcpy(h, host_out, h->prof, FM_NPROF * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     int khz = 0;
     HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
     host_out[PH_KHZ] = (uint64_t)khz;
   }
   if (mode == 1) {
-    HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemset(h->prof, 0, FM_NPROF * sizeof(unsigned long long)));
+    HIPCHK(d_sync(h));
+    HIPCHK(d_memset(h, h->prof, 0, FM_NPROF * sizeof(unsigned long long)));
     h->prof_on = true;
   } else if (mode == 0) {
     h->prof_on = false;
@@ -1058,25 +1158,25 @@ int fm_profile(fm_handle* h, int mode, uint64_t* host_out) {
 
 int fm_get_counters(fm_handle* h, int64_t* host_out) {
   if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(host_out, h->counters, (size_t)h->dm.N * FM_NCTR * sizeof(int64_t), hipMemcpyDeviceToHost));
+  HIPCHK(d_setdev(h));
+  HIPCHK(d_sync(h));
+  HIPCHK(d_memcpy(h, host_out, h->counters, (size_t)h->dm.N * FM_NCTR * sizeof(int64_t), hipMemcpyDeviceToHost));
   return FM_OK;
 }
 
 int fm_get_costs(fm_handle* h, uint32_t* host_out) {
   if (!h || !host_out) return set_err(FM_EINVAL, "null argument");
   if (!h->cost) return set_err(FM_EINVAL, "no per-arena costs (FACTORYSIM_NO_LPT)");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpy(host_out, h->cost, (size_t)h->dm.N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(d_setdev(h));
+  HIPCHK(d_sync(h));
+  HIPCHK(d_memcpy(h, host_out, h->cost, (size_t)h->dm.N * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return FM_OK;
 }
 
 int fm_kernel_timing(fm_handle* h, int enable) {
   if (!h) return set_err(FM_EINVAL, "null handle");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(d_setdev(h));
+  HIPCHK(d_sync(h));
   ktime_clear(h);
   h->ktime_on = enable != 0;
   return FM_OK;
@@ -1084,8 +1184,8 @@ int fm_kernel_timing(fm_handle* h, int enable) {
 
 int fm_get_kernel_time(fm_handle* h, double* total_ms, int* launches) {
   if (!h || !total_ms || !launches) return set_err(FM_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(d_setdev(h));
+  HIPCHK(d_sync(h));
   double t = 0.0;
   for (auto& e : h->ktime) {
     float ms = 0.0f;
@@ -1103,6 +1203,7 @@ int fm_render_ngeom(const fm_handle* h) { return h ? h->dm.ngc : -1; }
 int fm_render(fm_handle* h, const int32_t* arenas, int count, int width, int height, const float* camera,
               uint8_t* rgb, float* geom_frames) {
   if (!h || !arenas) return set_err(FM_EINVAL, "null argument");
+  if (h->cpu) return set_err(FM_EINVAL, "rendering is GPU-only");
   if (count < 0 || (count > 0 && (width < 1 || height < 1 || width > 8192 || height > 8192)))
     return set_err(FM_EINVAL, "bad image size");
   if (!rgb && !geom_frames) return set_err(FM_EINVAL, "nothing to write (rgb and geom_frames are both NULL)");
@@ -1110,27 +1211,27 @@ int fm_render(fm_handle* h, const int32_t* arenas, int count, int width, int hei
   for (int i = 0; i < count; i++)
     if (arenas[i] < 0 || arenas[i] >= h->dm.N) return set_err(FM_EINVAL, "arena index out of range");
   if (count == 0) return FM_OK;
-  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(d_setdev(h));
   if (!h->render_rgb) {
     std::vector<float> c = render_colours(h->sc);
-    HIPCHK(hipMalloc((void**)&h->render_rgb, c.size() * sizeof(float)));
-    HIPCHK(hipMemcpy(h->render_rgb, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc((void**)&h->cube_rgba, h->sc.cube_rgba.size() * sizeof(float)));
-    HIPCHK(hipMemcpy(h->cube_rgba, h->sc.cube_rgba.data(), h->sc.cube_rgba.size() * sizeof(float),
+    HIPCHK(d_malloc(h, (void**)&h->render_rgb, c.size() * sizeof(float)));
+    HIPCHK(d_memcpy(h, h->render_rgb, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(d_malloc(h, (void**)&h->cube_rgba, h->sc.cube_rgba.size() * sizeof(float)));
+    HIPCHK(d_memcpy(h, h->cube_rgba, h->sc.cube_rgba.data(), h->sc.cube_rgba.size() * sizeof(float),
                      hipMemcpyHostToDevice));
   }
   if (!h->render_copied) HIPCHK(hipEventCreateWithFlags(&h->render_copied, hipEventDisableTiming));
   if ((size_t)count > h->render_cap) {
     // growing the scratch frees buffers queued work may still read: the one synchronising path (rare)
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(d_sync(h));
     if (h->render_frames) HIPCHK(hipFree(h->render_frames));
     if (h->render_arenas) HIPCHK(hipFree(h->render_arenas));
     if (h->render_arenas_host) HIPCHK(hipHostFree(h->render_arenas_host));
     h->render_frames = nullptr;
     h->render_arenas = nullptr;
     h->render_arenas_host = nullptr;
-    HIPCHK(hipMalloc((void**)&h->render_frames, (size_t)count * h->dm.ngc * RF_N * sizeof(float)));
-    HIPCHK(hipMalloc((void**)&h->render_arenas, (size_t)count * sizeof(int)));
+    HIPCHK(d_malloc(h, (void**)&h->render_frames, (size_t)count * h->dm.ngc * RF_N * sizeof(float)));
+    HIPCHK(d_malloc(h, (void**)&h->render_arenas, (size_t)count * sizeof(int)));
     HIPCHK(hipHostMalloc((void**)&h->render_arenas_host, (size_t)count * sizeof(int), hipHostMallocDefault));
     h->render_cap = count;
   } else {

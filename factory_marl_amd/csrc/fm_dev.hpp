@@ -1,6 +1,10 @@
 // fm_dev.hpp -- device-side data structures and small math helpers for the env-step kernel.
 #pragma once
+#ifdef FM_HOST_SIMT
+#include "fm_simt_host.hpp"  // the CPU backend: this code compiled for the host, the wave emulated (fm_cpu.cpp)
+#else
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cstdint>
 
@@ -20,6 +24,14 @@ namespace fm {
 #define FM_AS_CONST
 #define FM_AS_GLOBAL
 #define FM_AS(n)
+#endif
+// an opaque copy of a value the compiler must not hoist or fold (uniform "s" / per-lane "v" register classes on the GPU)
+#ifdef FM_HOST_SIMT
+#define FM_OPAQUE_S(x) asm volatile("" : "+r"(x))
+#define FM_OPAQUE_V(x) asm volatile("" : "+r"(x))
+#else
+#define FM_OPAQUE_S(x) asm volatile("" : "+s"(x))
+#define FM_OPAQUE_V(x) asm volatile("" : "+v"(x))
 #endif
 // address spaces by number (FM_AS(n)): 1 global, 3 LDS, 4 constant.  Non-inlined device functions take their
 // pointer parameters in a named address space: a plain pointer parameter is generic inside the callee, and every
@@ -204,7 +216,7 @@ struct StepIO {
 // loads through the same pointer (keeps long-lived launch parameters out of the SGPR file)
 template <typename P>
 __device__ __forceinline__ const P* opaque(const P* p) {
-  asm volatile("" : "+s"(p));
+  FM_OPAQUE_S(p);
   return p;
 }
 
@@ -212,9 +224,16 @@ __device__ __forceinline__ const P* opaque(const P* p) {
 template <typename P>
 __device__ __forceinline__ const P& kparams() {
   const P FM_AS_CONST* p = (const P FM_AS_CONST*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
+  FM_OPAQUE_S(p);
   return *(const P*)p;
 }
+
+// the kernel's dynamic LDS (the CPU backend: the emulated wave's per-thread buffer)
+#ifdef FM_HOST_SIMT
+#define FM_SMEM_DECL(name) char* name = ::fm_simt::wave().lds
+#else
+#define FM_SMEM_DECL(name) extern __shared__ __attribute__((aligned(16))) char name[]
+#endif
 
 // LDS base with an opaque zero VGPR added: every workspace access becomes [vbase + immediate offset]
 // instead of one hoisted SGPR per distinct LDS address (which the compiler otherwise keeps live across
@@ -224,7 +243,12 @@ __device__ __forceinline__ char* lds_base(char* smem) {
   return smem;
 #endif
   unsigned int z;
+#ifdef FM_HOST_SIMT
+  z = 0;
+  FM_OPAQUE_V(z);
+#else
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#endif
   return smem + z;
 }
 
@@ -532,7 +556,7 @@ __host__ __device__ constexpr int tb_floats(int ntree) { return tb_sol(ntree) + 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
                                               bool midcache = false, bool nobc = false, bool f64arms = false,
-                                              bool gl_lists = false, bool treeblk = false) {
+                                              bool gl_lists = false, bool treeblk = false, int tmask_words = 0) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -596,7 +620,9 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   if (!spill) L.c_r = take(tsize * CR_N * maxcon);
   L.r_i = take(4 * 4 * maxrow);
   L.r_r = take(tsize * RR_N * maxrow);
-  L.tmask = take(8 * ntree * ((maxcon + 63) / 64));  // word h of tree t at [h * ntree + t]
+  // word h of tree t at [h * ntree + t]; the readers (and the zero fill past maxcon) cover DIM::MAXC / 64 words
+  const int tmw = (maxcon + 63) / 64 > tmask_words ? (maxcon + 63) / 64 : tmask_words;
+  L.tmask = take(8 * ntree * tmw);
   L.misc = take(4 * (16 + WAVE));  // 16 scalars + the Hessian assembly's block offsets
   L.sort = take(4 * K);
   L.uctl = take(8 * nu);

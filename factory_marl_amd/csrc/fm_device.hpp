@@ -18,7 +18,9 @@
 // layer); everything with natural width runs across the wave (geoms, broadphase pairs, narrowphase,
 // contact rows, Hessian entries, Cholesky trailing updates, line-search reductions).
 #pragma once
+#ifndef FM_HOST_SIMT
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cmath>
 #include <type_traits>
@@ -61,13 +63,13 @@ __device__ __forceinline__ void static_for(F&& f) {
 // a uniform int the compiler must re-read at each use (not hoisted: see the record macros of step_arena)
 __device__ __forceinline__ int opaque_uniform(int x) {
   x = __builtin_amdgcn_readfirstlane(x);  // uniform by contract (one arena per wave)
-  asm volatile("" : "+s"(x));
+  FM_OPAQUE_S(x);
   return x;
 }
 __device__ __forceinline__ int lane_id() {
   int t = (int)threadIdx.x;
 #if FM_OPAQUE_LANE
-  asm volatile("" : "+v"(t));
+  FM_OPAQUE_V(t);
 #endif
   return t;
 }
@@ -2507,6 +2509,7 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     Ma[9 * i + j] = s;
     Ma[9 * j + i] = s;
   }
+  SYNC();  // collide's geom centres (gx) reuse the H scratch the loop above reads
   PMARK(PH_GEOM);
   collide(M, w, arena, ctr);
   int* misc = w.misc();
@@ -5633,7 +5636,7 @@ __device__ __forceinline__ void store_state(const Model<T>& M, const State<T>& S
 
 template <typename T, typename DIM>
 __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L, float* obs, const uint8_t* mask) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FM_SMEM_DECL(smem);
   const int arena = blockIdx.x;
   const DIM dm(M.dm);
   if (mask && !mask[arena]) return;
@@ -6014,7 +6017,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
 
 template <typename T, typename DIM, bool IK>
 __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> params) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FM_SMEM_DECL(smem);
   (void)params;
   if constexpr (DIM::rerun) {
     // the wide-capacity rerun: the arenas the 64-contact launch abandoned, S.rerun[1 + i] for i < S.rerun[0], over
@@ -6042,7 +6045,7 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
 template <typename T, typename DIM>
 __global__ void __launch_bounds__(64) debug_kernel(Model<T> M, State<T> S, Lay L, int arena, int actuated,
                                                    double* out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FM_SMEM_DECL(smem);
   const DIM dm(M.dm);
   Ws<T, DIM> w{lds_base(smem), &L, spill_base<DIM>(S, arena)};
   int64_t* ctr = S.counters + FM_NCTR * (size_t)arena;

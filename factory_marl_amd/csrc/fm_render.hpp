@@ -34,7 +34,7 @@ struct RenderParams {
 
 template <typename T, typename DIM>
 __global__ void __launch_bounds__(64) render_frames_kernel(Model<T> M, State<T> S, Lay L, RenderParams rp) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FM_SMEM_DECL(smem);
   const DIM dm(M.dm);
   Ws<T, DIM> w{lds_base(smem), &L};
   const int slot = blockIdx.x, arena = rp.arenas[slot];
@@ -189,7 +189,7 @@ __device__ __forceinline__ float cast_ray(const float* tab, int ngc, const float
 }
 
 __global__ void __launch_bounds__(64) render_pixels_kernel(RenderParams rp, int ngc) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FM_SMEM_DECL(smem);
   float* tab = (float*)smem;
   const int slot = blockIdx.y;
   const float* src = rp.frames + (size_t)slot * ngc * RF_N;

@@ -153,9 +153,14 @@ class FactoryVecEnv:
             raise ValueError("need one seed per arena")
         self.seeds_used = seeds.copy()
         self.env_kwargs = kw
+        # device: a GPU index / "cuda:i", or "cpu" / -1 for the CPU backend (fm_create device = -1: the kernel's own
+        # sources on host threads, every buffer a CPU tensor; BASELINE config 1)
+        if isinstance(device, int) and device < 0:
+            device = "cpu"
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.cpu = self.device.type == "cpu"
         h = C.c_void_p()
-        _lib.check(L.fm_create(C.byref(cfg), self.device.index or 0,
+        _lib.check(L.fm_create(C.byref(cfg), -1 if self.cpu else (self.device.index or 0),
                                seeds.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(h)))
         self._h = h
         self._L = L
@@ -199,6 +204,8 @@ class FactoryVecEnv:
     # ------------------------------------------------------------------ core API
     def _bind_stream(self):
         """run on torch's current stream so action / observation tensors are ordered with torch work"""
+        if self.cpu:
+            return
         s = self.torch.cuda.current_stream(self.device)
         if self._stream_bound != s.cuda_stream:
             _lib.check(self._L.fm_set_stream(self._h, C.c_void_p(s.cuda_stream) if s.cuda_stream else None))
@@ -476,7 +483,8 @@ class FactoryVecEnv:
 
     def set_state(self, buf):
         self._bind_stream()
-        self.torch.cuda.synchronize(self.device)
+        if not self.cpu:
+            self.torch.cuda.synchronize(self.device)
         buf = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
         _lib.check(self._L.fm_set_state(self._h, buf.ctypes.data_as(C.c_void_p)))
 

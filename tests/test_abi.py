@@ -103,3 +103,39 @@ def test_state_record_roundtrip():
     assert f["qpos"].shape == (nq,) and f["ctrl_target"].shape == (nu,) and f["episode_return"].shape == (1,)
     # sizes of the benchmark scene (nq 47, nv 43, nu 17, obs 100)
     assert (nq, nv, nu) == (47, 43, 17)
+
+
+def test_config1_steps_on_the_cpu_backend_and_matches_the_oracle(lib, oracle):
+    """BASELINE config 1 (one env, 2 arms x 4 objects, random policy -- the reference's visualisation.py:32-77 loop)
+    through the same C ABI on device = -1 (the kernel's own sources on the host, fm_cpu.cpp): started from the
+    oracle's reset record, 30 free-running env-steps against the oracle's; fp64, state within 1e-6 relative,
+    task integers / RNG / flags bit for bit"""
+    import torch
+
+    from factory_marl_amd import FactoryVecEnv, state as st
+    from factory_marl_amd.environments import run_kwargs
+
+    A, K = 2, 4
+    e = oracle.Env(A, K, 42, weights=(0.2, 0.4, 0.1, 0.4))
+    e.reset()
+    kw = run_kwargs("AllFullRLProgressRewardEnv", num_arms=A, max_num_objects=K, seed=42)
+    kw["small_action_norm_reward_factor"] = 0.1
+    env = FactoryVecEnv(1, env_kwargs=kw, device=-1, precision="fp64")
+    env.reset()
+    env.set_state(st.pack(A, K, *e.export_state())[None])
+    rng = np.random.default_rng(1)
+    for t in range(30):
+        a = rng.uniform(-1, 1, 8 * A).astype(np.float32)
+        obs, rew, term, _, _ = e.step(a)
+        g_obs, g_rew, g_term, _ = env.step_tensors(torch.as_tensor(a[None]))
+        assert bool(g_term[0]) == term, t
+        assert float(g_rew[0]) == pytest.approx(rew, abs=1e-6), t
+        assert np.abs(g_obs[0].numpy() - obs).max() <= 1e-5, t
+        gd, gi, gr = st.unpack(A, K, env.get_state()[0])
+        d, i, r = e.export_state()
+        assert np.array_equal(gi, i) and np.array_equal(gr, r), t
+        qd, vd = __import__("parity_util").state_err(A, K, gd, d)
+        assert max(qd.max(), vd.max()) <= 1e-6, (t, qd.max(), vd.max())
+        if term:
+            break
+    env.close()

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""LDS race check of the env-step kernel on the CPU backend (test/measurement infra, CPU only).
+
+The kernel's lanes hand data to each other through LDS at SYNC() (fm_device.hpp).  On the GPU one wave executes in
+lockstep, so a hand-off that lacks the barrier still works there; the CPU backend runs the 64 lanes of a wave one
+after another between cross-lane points (fm_simt_host.hpp), where it does not.  This tool runs the CPU backend built
+with the race detector (fm_cpu.cpp FM_RACE_DETECT: the TSan instrumentation hooks, a shadow word per 4 bytes of LDS)
+over a few env-steps of each env class and prints every pair of source lines where two lanes touched the same LDS
+word between two rendezvous with at least one write (RAW / WAR / WAW), symbolized with llvm-symbolizer.
+
+usage: tools/lds_race_check.sh   (builds factory_marl_amd/lib_race.so, then runs this with FACTORYSIM_LIB set)"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.environments import run_kwargs
+
+    cases = [("AllFullRLProgressRewardEnv", 2, 4), ("PauseIKToggleEnv", 2, 4), ("AllDeltaProgressRewardEnv", 2, 4),
+             ("AllFullRLProgressRewardEnv", 2, 8)]
+    steps = int(os.environ.get("RACE_STEPS", "3"))
+    if os.environ.get("RACE_CASES"):
+        cases = [cases[int(i)] for i in os.environ["RACE_CASES"].split(",")]
+    for prec in os.environ.get("RACE_PRECISIONS", "fp64,fp32").split(","):
+        for cls, A, K in cases:
+            env = FactoryVecEnv(1, env_class=cls, env_kwargs=run_kwargs(cls, num_arms=A, max_num_objects=K, seed=42),
+                                device="cpu", precision=prec)
+            env.reset()
+            rng = np.random.default_rng(0)
+            for _ in range(steps):
+                if cls in ("PauseIKToggleEnv", "BackupIKToggleEnv"):
+                    a = (rng.random((1, env.act_dim)) < 0.5).astype(np.float32)
+                else:
+                    a = rng.uniform(-1, 1, (1, env.act_dim)).astype(np.float32)
+                env.step(a)
+            env.close()
+            print(f"ran {prec} {cls} ({A},{K}) x {steps}", flush=True)
+    lib = os.environ["FACTORYSIM_LIB"]
+    L = C.CDLL(lib)
+    buf = C.create_string_buffer(1 << 20)
+    n = L.fm_race_report(buf, len(buf))
+    text = buf.value.decode().split("\n", 1)
+    lay = [int(x) for x in text[0].split()[1:]]
+    lines = text[1].split()
+    print(f"{n} racing access pairs")
+    kinds = {"0": "RAW", "1": "WAR", "2": "WAW"}
+    recs = [(kinds[lines[i]], lines[i + 1], lines[i + 2], int(lines[i + 3])) for i in range(0, len(lines), 4)]
+    names = lay_names()
+    sym = os.path.join("/opt/rocm/lib/llvm/bin", "llvm-symbolizer")
+    allpc = sorted({pc for _, a, b, _ in recs for pc in (a, b)})
+    out = subprocess.run([sym, "--obj", lib, "--inlining", "--functions=short"] + allpc, capture_output=True,
+                         text=True).stdout
+    blocks = [b.strip().splitlines() for b in out.strip().split("\n\n")]
+
+    def site(blk):
+        # (function, file:line) pairs innermost first; an optimised-away line (":0:") takes its caller's line
+        frames = [(blk[i], blk[i + 1].split("csrc/")[-1]) for i in range(0, len(blk) - 1, 2)]
+        for fn, loc in frames:
+            if ":0:" not in loc:
+                return f"{loc} ({fn})"
+        return frames[0][1] if frames else "?"
+
+    where = {pc: site(blk) for pc, blk in zip(allpc, blocks)}
+    seen = set()
+    for kind, a, b, off in recs:
+        k = (kind, where[a], where[b])
+        if k in seen:
+            continue
+        seen.add(k)
+        print(f"{kind}: {where[a]}  <->  {where[b]}   [{region(off, names, lay)}]")
+
+
+def lay_names():
+    """the int fields of struct Lay (fm_dev.hpp), in order"""
+    import re
+    src = open(os.path.join(ROOT, "factory_marl_amd/csrc/fm_dev.hpp")).read()
+    body = src[src.index("struct Lay {") + 12:]
+    body = body[:body.index("};")]
+    body = re.sub(r"//[^\n]*", "", body)
+    return [n.strip() for decl in body.split(";") if decl.strip().startswith("int ")
+            for n in decl.strip()[4:].split(",")]
+
+
+def region(off, names, lay):
+    if off < 0:
+        return "global"
+    if not lay:
+        return f"LDS +{off}"
+    best = max(((v, n) for n, v in zip(names, lay) if 0 <= v <= off), default=(0, "?"))
+    return f"LDS +{off} = {best[1]} +{off - best[0]}"
+
+
+if __name__ == "__main__":
+    main()
