@@ -2768,24 +2768,51 @@ __device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T, DIM>& w, int
   }
 }
 
+// 1 / sqrt(s) in float64 for a pivot: v_rsq_f64 refined by two Newton steps (~1 ulp) -- a dependent chain of 7
+// operations where sqrt() then a division is ~20 (both expand to refinement sequences)
+__device__ __forceinline__ double rsqrt_f64(double s) {
+#ifdef FM_HOST_SIMT
+  return 1.0 / sqrt(s);
+#else
+  double y = __builtin_amdgcn_rsq(s);
+  const double h = 0.5 * s;
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  return y;
+#endif
+}
+__device__ __forceinline__ float rsqrt_f64(float s) { return 1.0f / sqrtf(s); }
+// a pivot's reciprocal square root in the factor's precision
+template <typename T>
+__device__ __forceinline__ T rsqrt_div(T d) {
+  if constexpr (sizeof(T) == 4)
+    return 1.0f / sqrtf(d);
+  else
+    return rsqrt_f64(d);
+}
+
 // 9x9 SPD solve A x = b on one lane with A's lower triangle (packed row-major, P9(i,j) = i(i+1)/2 + j)
 // held in registers (right-looking factor, then forward and backward substitution)
 __host__ __device__ constexpr int P9(int i, int j) { return i * (i + 1) / 2 + j; }
 template <typename T>
 __device__ __forceinline__ void spd9_solve(T (&A)[45], T (&x)[9]) {
+  // the pivots' reciprocal square roots and multiplications instead of a square root and a division per column and a
+  // division per entry: a float64 division or square root is a ~10-instruction dependent sequence, and the
+  // substitutions below were a chain of 18 divisions (integration 6.1 -> 4.7, smooth 5.8 -> 4.4 us per arena-substep
+  // for the reciprocal alone, profiles/r05i_phase_fp32.json)
+  T inv[9];
 #pragma unroll
   for (int j = 0; j < 9; j++) {
     T s = A[P9(j, j)];
 #pragma unroll
     for (int k = 0; k < j; k++) s -= A[P9(j, k)] * A[P9(j, k)];
-    const T l = sqrt(s > T(1e-300) ? s : T(1e-300));
-    A[P9(j, j)] = l;
+    inv[j] = rsqrt_f64(s > T(1e-300) ? s : T(1e-300));
 #pragma unroll
     for (int i = j + 1; i < 9; i++) {
       T t = A[P9(i, j)];
 #pragma unroll
       for (int k = 0; k < j; k++) t -= A[P9(i, k)] * A[P9(j, k)];
-      A[P9(i, j)] = t / l;
+      A[P9(i, j)] = t * inv[j];
     }
   }
 #pragma unroll
@@ -2793,14 +2820,14 @@ __device__ __forceinline__ void spd9_solve(T (&A)[45], T (&x)[9]) {
     T t = x[i];
 #pragma unroll
     for (int k = 0; k < i; k++) t -= A[P9(i, k)] * x[k];
-    x[i] = t / A[P9(i, i)];
+    x[i] = t * inv[i];
   }
 #pragma unroll
   for (int i = 8; i >= 0; i--) {
     T t = x[i];
 #pragma unroll
     for (int k = i + 1; k < 9; k++) t -= A[P9(k, i)] * x[k];
-    x[i] = t / A[P9(i, i)];
+    x[i] = t * inv[i];
   }
 }
 
@@ -2966,7 +2993,7 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
     constexpr int tk = k == NV - 1 ? 0 : (k < A0 - 1 ? 1 + k / 6 : 1 + KK + (k - (A0 - 1)) / 9);
     T d = readlane(col[k], k);
     d = d > tiny ? d : tiny;
-    const T ri = T(1) / sqrt(d);
+    const T ri = rsqrt_div(d);
     const T lj = col[k] * ri;
     if (j == k) dinv = ri;
     if (j >= k) col[k] = lj;
@@ -3141,7 +3168,7 @@ __device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM
     const int p = (ps + s) & (WAVE - 1);
     T d = __shfl(loc[s], p);
     d = d > tiny ? d : tiny;
-    const T ri = T(1) / sqrt(d);
+    const T ri = rsqrt_div(d);
     const T lj = loc[s] * ri;           // L[j][k] (j >= k)
     const T lb = __shfl(bel, p) * ri;   // L[belt][k]
     if (act && jl == s) {
@@ -3167,7 +3194,7 @@ __device__ __forceinline__ void chol_arrow_rl(const Model<T>& M, const Ws<T, DIM
     db -= x * x;
   }
   db = db > tiny ? db : tiny;
-  const T rib = T(1) / sqrt(db);
+  const T rib = rsqrt_div(db);
   // forward: L y = -g
   T acc = blk ? (T)-g[jo] : T(0);
   T y = T(0);
@@ -3249,7 +3276,7 @@ __device__ __forceinline__ void chol_arrow2_rl(const T* H, const double* g, T* d
       const int p = (ps[P] + s) & (WAVE - 1);
       T d = __shfl(loc[P][s], p);
       d = d > tiny ? d : tiny;
-      const T ri = T(1) / sqrt(d);
+      const T ri = rsqrt_div(d);
       const T lj = loc[P][s] * ri;
       const T lb = __shfl(bel[P], p) * ri;
       if (act && jl[P] == s) {
@@ -3280,7 +3307,7 @@ __device__ __forceinline__ void chol_arrow2_rl(const T* H, const double* g, T* d
     db -= x * x;
   }
   db = db > tiny ? db : tiny;
-  const T rib = T(1) / sqrt(db);
+  const T rib = rsqrt_div(db);
   T y[2];
   T accb = (T)-g[0];
 #pragma unroll
@@ -3557,7 +3584,7 @@ __device__ __forceinline__ bool chol_sparse_lds(const Model<T>& M, const Ws<T, D
     const unsigned ak = (unsigned)__builtin_amdgcn_readlane((int)adj, tk) | (1u << tk);
     T d = H[dk * HS + dk];
     d = d > tiny ? d : tiny;
-    const T ri = T(1) / sqrt(d);
+    const T ri = rsqrt_div(d);
     int m = 0;
     for (int p0 = k + 1; p0 < NV; p0 += WAVE) {
       const int p = p0 + LANE;
@@ -3859,7 +3886,7 @@ __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const 
       SYNC();
       T d = bc[k];
       d = d > tiny ? d : tiny;
-      const T ri = T(1) / sqrt(d);
+      const T ri = rsqrt_div(d);
       const T lj = col[k] * ri;
       if (j == k) dinv = ri;
       if (j >= k) col[k] = lj;
@@ -3902,13 +3929,6 @@ __device__ __forceinline__ void chol_solve_reg(const T* H, T* bc, int nv, const 
 // wave barriers per pivot -- the system is one small dense block solved once per Newton iteration
 // (T = double: the fp64 tree-block solve; the pivot broadcasts go through lane_bcast, ds_bpermute for 64-bit values
 // -- see the 64-bit cross-lane hazard)
-template <typename T>
-__device__ __forceinline__ T rsqrt_div(T d) {
-  if constexpr (sizeof(T) == 4)
-    return 1.0f / sqrtf(d);
-  else
-    return 1.0 / sqrt(d);
-}
 template <int NVM, typename T = float>
 __device__ __forceinline__ void chol_solve_rl(const T* H, int nv, const double* g, T* dir) {
   const int j = LANE;
