@@ -22,7 +22,7 @@ hipError_t rerun_set_attr();
 template <typename T, int A, int K>
 Lay rerun_layout();
 template <typename T, int A, int K>
-void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik);
+void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik, bool concurrent);
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes);
 template <typename T, int A, int K>
@@ -68,6 +68,17 @@ static int set_err(int code, const std::string& msg) {
   do {                                                                                             \
     hipError_t e_ = (x);                                                                           \
     if (e_ != hipSuccess) return set_err(FM_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// inside a launch sequence (void): a failed event record / wait falls back to a device-wide synchronisation, which
+// orders the two streams' work as the event would have
+#define HIPCHKV(x)                                                                                 \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) {                                                                        \
+      fprintf(stderr, "factorysim: %s: %s\n", #x, hipGetErrorString(e_));                          \
+      (void)hipDeviceSynchronize();                                                                \
+    }                                                                                              \
   } while (0)
 
 struct fm_handle {
@@ -129,6 +140,10 @@ struct fm_handle {
   // the benchmark scene's lossless contacts: [1 + N] rerun list of the 64-contact launch (fm_dev.hpp State::rerun),
   // the IK classes' record backup, the wide kernel's layout
   int32_t* rerun = nullptr;
+  // concurrent rerun: the wide kernel runs on a side stream alongside the 64-contact launch (State::rdone)
+  int32_t* rdone = nullptr;
+  hipStream_t rstream = nullptr;
+  hipEvent_t rev_start = nullptr, rev_end = nullptr;
   char* bak = nullptr;
   double* resume = nullptr;    // [N][resume_stride] substep state of an abandoned env-step
   Lay lay_rerun{};
@@ -266,7 +281,7 @@ static Model<T> make_model(const fm_handle* h) {
 // experiment switches of the kernel (A/B probes and the equivalence tests; every default is 0): read from the
 // environment once, at fm_create, and reported on stderr when any is set; "experiment_flags" (fm_set_param) changes
 // them on a live handle for later launches
-constexpr uint32_t FM_XFLAGS_MASK = 0x7FFFu;  // the switches below (fm_set_param rejects other bits)
+constexpr uint32_t FM_XFLAGS_MASK = 0xFFFFu;  // the switches below (fm_set_param rejects other bits)
 static uint32_t read_experiment_flags() {
   struct Sw {
     const char* var;
@@ -289,6 +304,7 @@ static uint32_t read_experiment_flags() {
       {"FM_PC_SCATTER", '1', 4096},    // (2,4): J' f by the per-contact scatter instead of per (contact, column)
       {"FM_TB_LDSBC", '1', 8192},      // tree-block solve: its coupled system by the LDS-broadcast register factor
       {"FM_RERUN_AT_50", '1', 16384},  // (2,4): every env-step abandoned at substep 50, resumed there by the wide kernel
+      {"FM_CONCURRENT_RERUN", '1', 32768},  // (2,4): the wide kernel alongside the 64-contact launch (side stream)
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {
@@ -533,6 +549,11 @@ static int create_typed(fm_handle* h) {
     HIPCHK(d_malloc(h, (void**)&h->rerun, (N + 1) * sizeof(int32_t)));
     h->allocs.push_back(h->rerun);
     HIPCHK(d_memset(h, h->rerun, 0, (N + 1) * sizeof(int32_t)));
+    HIPCHK(d_malloc(h, (void**)&h->rdone, sizeof(int32_t)));
+    h->allocs.push_back(h->rdone);
+    HIPCHK(hipStreamCreateWithFlags(&h->rstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&h->rev_start, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&h->rev_end, hipEventDisableTiming));
     // the substep state of an abandoned env-step (the wide kernel resumes from it, fm_dev.hpp State::resume)
     HIPCHK(d_malloc(h, (void**)&h->resume, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
     h->allocs.push_back(h->resume);
@@ -648,15 +669,17 @@ __global__ void __launch_bounds__(1024) lpt_order_kernel(const uint32_t* __restr
 // the wide-capacity rerun of the arenas the 64-contact launch abandoned (one workgroup per arena of the handle;
 // the ones past the list's count exit at once)
 template <typename T>
-static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik) {
+static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik, hipStream_t stream, bool concurrent) {
   StepParams<T> pr = pd;
   pr.L = h->lay_rerun;
   pr.S.order = nullptr;
   pr.S.rerun = h->rerun;
   pr.S.bak = h->bak;
   pr.S.resume = h->resume;
+  pr.S.rdone = concurrent ? h->rdone : nullptr;
+  pr.S.rdone_of = h->dm.N;
   pr.M.dm.maxcon = MAXCON_WIDE;  // the wide kernel keeps up to 128 contacts per stage
-  rerun_launch<T, 2, 4>(pr, h->dm.N, h->stream, ik);
+  rerun_launch<T, 2, 4>(pr, h->dm.N, stream, ik, concurrent);
 }
 
 // kernel-only timing (fm_kernel_timing): a HIP event pair on the handle's stream around each env-step kernel launch
@@ -688,8 +711,12 @@ static void launch_step(fm_handle* h, const StepIO& io) {
   }
   if (h->order) hipLaunchKernelGGL(lpt_order_kernel, dim3(1), dim3(1024), 0, h->stream, h->cost, h->order, h->dm.N);
   bool rerun = h->rerun && !(h->xflags & 1024);
-  if (rerun && hipMemsetAsync(h->rerun, 0, sizeof(int32_t), h->stream) != hipSuccess) {
-    // a stale count would make the rerun kernel re-step the previous launch's abandoned arenas: run without the
+  // FM_CONCURRENT_RERUN=1: the wide kernel waits on a side stream and takes each abandoned arena as it is published
+  // (measured 9 % slower than the serial rerun -- any resident second kernel slowed the launch)
+  const bool concurrent = rerun && h->rstream && (h->xflags & 32768);
+  if (rerun && (hipMemsetAsync(h->rerun, 0, (h->dm.N + 1) * sizeof(int32_t), h->stream) != hipSuccess ||
+                (concurrent && hipMemsetAsync(h->rdone, 0, sizeof(int32_t), h->stream) != hipSuccess))) {
+    // a stale list would make the rerun kernel re-step the previous launch's abandoned arenas: run without the
     // rerun list instead (stages above 64 contacts are then cut and counted in counters[0])
     fprintf(stderr, "factorysim: clearing the rerun list failed; this launch cuts contacts above 64\n");
     rerun = false;
@@ -708,10 +735,24 @@ static void launch_step(fm_handle* h, const StepIO& io) {
       pf.S.bak = h->bak;                                                                               \
       pf.S.resume = h->resume;                                                                         \
     }                                                                                                  \
+    if (concurrent) {                                                                                  \
+      /* the wide kernel on the side stream, queued before the 64-contact launch; the handle's stream \
+         waits for it before the next work */                                                          \
+      pf.S.rdone = h->rdone;                                                                           \
+      pf.S.rdone_of = h->dm.N;                                                                         \
+      HIPCHKV(hipEventRecord(h->rev_start, h->stream));                                                \
+      HIPCHKV(hipStreamWaitEvent(h->rstream, h->rev_start, 0));                                        \
+      launch_rerun<T>(h, pd, ik, h->rstream, true);                                                    \
+    }                                                                                                  \
     ktime_begin(h);                                                                                    \
     fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream, ik);                              \
     ktime_end(h);                                                                                      \
-    if (rerun) launch_rerun<T>(h, pd, ik);                                                             \
+    if (concurrent) {                                                                                  \
+      HIPCHKV(hipEventRecord(h->rev_end, h->rstream));                                                 \
+      HIPCHKV(hipStreamWaitEvent(h->stream, h->rev_end, 0));                                           \
+    } else if (rerun) {                                                                                \
+      launch_rerun<T>(h, pd, ik, h->stream, false);                                                    \
+    }                                                                                                  \
     return;                                                                                            \
   }                                                                                                    \
   idx++;
@@ -925,6 +966,12 @@ void fm_destroy(fm_handle* h) {
   if (h->render_arenas_host) (void)hipHostFree(h->render_arenas_host);
   if (h->render_copied) (void)hipEventDestroy(h->render_copied);
   if (h->handoff) (void)hipEventDestroy(h->handoff);
+  if (h->rstream) {
+    (void)hipStreamSynchronize(h->rstream);
+    (void)hipStreamDestroy(h->rstream);
+  }
+  if (h->rev_start) (void)hipEventDestroy(h->rev_start);
+  if (h->rev_end) (void)hipEventDestroy(h->rev_end);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);  // never a stream the caller handed in
   delete h;
 }

@@ -169,9 +169,15 @@ struct State {
   // DimsSpill: per-arena global scratch blocks (Lay::gtotal bytes each) for the Hessian and the contact records
   gptr<char> spill{nullptr};
   long long spill_stride{0};
-  // (2,4) contact overflow: [0] = count, [1 + i] = arena ids whose env-step the 64-contact kernel abandoned (its
-  // record untouched) for the wide rerun kernel.  Null: the capacity cut (counted in counters[0]) instead
+  // (2,4) contact overflow: [0] = count, [1 + i] = 1 + the arena ids whose env-step the 64-contact kernel abandoned
+  // (0: slot not yet written) for the wide rerun kernel.  Null: the capacity cut (counted in counters[0]) instead
   gptr<int32_t> rerun{nullptr};
+  // concurrent rerun: the 64-contact launch's finished workgroups (each adds 1 after its arena, abandoned or not).
+  // The wide kernel, launched on a second stream alongside, takes each abandoned arena as soon as it is published and
+  // ends once all `rdone_of` workgroups are done and every published slot is taken (FM_CONCURRENT_RERUN=1, an
+  // experiment).  Null: the wide kernel runs after the launch (the default, serial rerun)
+  gptr<int32_t> rdone{nullptr};
+  int rdone_of{0};
   // IK classes with `rerun`: the arena's task records (dbl, ints) as the env-step found them, restored by the rerun
   // (the IK compose writes the FSM and the toggles' last actions before the substeps)
   gptr<char> bak{nullptr};
@@ -184,9 +190,11 @@ struct State {
 // doubles per arena of State::resume
 __host__ __device__ constexpr int resume_stride(int nq, int nv, int nu) { return 3 + nq + 2 * nv + 2 * nu; }
 
-// the arena's global scratch block (nullptr unless the kernel runs a DimsSpill layout)
+// the arena's global scratch block (nullptr unless the kernel runs a DimsSpill layout; the (2,4) wide rerun kernel
+// keeps its workspace in LDS, so it never touches the 64-contact launch's blocks while running alongside it)
 template <typename DIM, typename T>
 __device__ __forceinline__ char* spill_base(const State<T>& S, int arena) {
+  static_assert(!(DIM::spill && DIM::rerun), "a spilled wide rerun kernel would need scratch blocks of its own");
   if constexpr (DIM::spill)
     return (char*)S.spill + (long long)arena * S.spill_stride;
   else

@@ -599,6 +599,29 @@ __device__ __forceinline__ int dof_tree(const DD& d, int i) {
 __device__ __forceinline__ void sincos_t(float x, float* s, float* c) { sincosf(x, s, c); }
 __device__ __forceinline__ void sincos_t(double x, double* s, double* c) { sincos(x, s, c); }
 
+// 1 / sqrt(s) in float64 for a pivot: v_rsq_f64 refined by two Newton steps (~1 ulp) -- a dependent chain of 7
+// operations where sqrt() then a division is ~20 (both expand to refinement sequences)
+__device__ __forceinline__ double rsqrt_f64(double s) {
+#ifdef FM_HOST_SIMT
+  return 1.0 / sqrt(s);
+#else
+  double y = __builtin_amdgcn_rsq(s);
+  const double h = 0.5 * s;
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  return y;
+#endif
+}
+__device__ __forceinline__ float rsqrt_f64(float s) { return 1.0f / sqrtf(s); }
+// a pivot's reciprocal square root in the factor's precision
+template <typename T>
+__device__ __forceinline__ T rsqrt_div(T d) {
+  if constexpr (sizeof(T) == 4)
+    return 1.0f / sqrtf(d);
+  else
+    return rsqrt_f64(d);
+}
+
 template <typename T>
 __device__ __forceinline__ T impedance(const T* si, T x) {
   T dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
@@ -807,9 +830,10 @@ __device__ __forceinline__ bool bb_axis(int ax, const V3<T> (&A)[3], const V3<T>
   } else {
     const int i = (ax - 6) / 3, j = (ax - 6) % 3;
     u = vcross(vpick(i, A[0], A[1], A[2]), vpick(j, B[0], B[1], B[2]));
-    T n = sqrt(vdot(u, u));
-    if (n < T(1e-6)) return false;
-    u = V3<T>{u.x / n, u.y / n, u.z / n};
+    const T n2 = vdot(u, u);
+    if (n2 < T(1e-12)) return false;  // |u| < 1e-6
+    const T ri = rsqrt_f64(n2);       // one reciprocal square root instead of a square root and three divisions
+    u = V3<T>{u.x * ri, u.y * ri, u.z * ri};
   }
   T ra = h1[0] * fabs(vdot(u, A[0])) + h1[1] * fabs(vdot(u, A[1])) + h1[2] * fabs(vdot(u, A[2]));
   T rb = h2[0] * fabs(vdot(u, B[0])) + h2[1] * fabs(vdot(u, B[1])) + h2[2] * fabs(vdot(u, B[2]));
@@ -2768,28 +2792,6 @@ __device__ __forceinline__ void mmul(const Model<T>& M, const Ws<T, DIM>& w, int
   }
 }
 
-// 1 / sqrt(s) in float64 for a pivot: v_rsq_f64 refined by two Newton steps (~1 ulp) -- a dependent chain of 7
-// operations where sqrt() then a division is ~20 (both expand to refinement sequences)
-__device__ __forceinline__ double rsqrt_f64(double s) {
-#ifdef FM_HOST_SIMT
-  return 1.0 / sqrt(s);
-#else
-  double y = __builtin_amdgcn_rsq(s);
-  const double h = 0.5 * s;
-  y = fma(y, fma(-h * y, y, 0.5), y);
-  y = fma(y, fma(-h * y, y, 0.5), y);
-  return y;
-#endif
-}
-__device__ __forceinline__ float rsqrt_f64(float s) { return 1.0f / sqrtf(s); }
-// a pivot's reciprocal square root in the factor's precision
-template <typename T>
-__device__ __forceinline__ T rsqrt_div(T d) {
-  if constexpr (sizeof(T) == 4)
-    return 1.0f / sqrtf(d);
-  else
-    return rsqrt_f64(d);
-}
 
 // 9x9 SPD solve A x = b on one lane with A's lower triangle (packed row-major, P9(i,j) = i(i+1)/2 + j)
 // held in registers (right-looking factor, then forward and backward substitution)
@@ -5882,8 +5884,13 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
             }
           }
           if (LANE == 0) {
+            // publish: the slot's store releases the resume record and the backup at device scope (the wide kernel
+            // may be running on another stream, on another XCD, and takes the slot as soon as it is nonzero)
             int32_t* const rr = S.rerun;
-            rr[1 + atomicAdd(rr, 1)] = arena;
+            const int slot = atomicAdd(rr, 1);
+            __hip_atomic_store(rr + 1 + slot, arena + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            // ... and is ordered before this workgroup's (relaxed) count of finished workgroups
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           }
           return;
         }
@@ -6040,13 +6047,44 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
   FM_SMEM_DECL(smem);
   (void)params;
   if constexpr (DIM::rerun) {
-    // the wide-capacity rerun: the arenas the 64-contact launch abandoned, S.rerun[1 + i] for i < S.rerun[0], over
-    // the launch's workgroups (a small grid: the list is short, usually empty)
-    const int32_t* const rr = kparams<StepParams<T>>().S.rerun;
-    const int n = rr[0];
-    for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
-      step_arena<T, DIM, IK>(smem, rr[1 + i]);
-      FULL_SYNC();
+    // the wide-capacity rerun: the arenas the 64-contact launch abandoned, S.rerun[1 + i] - 1 for i < S.rerun[0],
+    // over the launch's workgroups (a small grid: the list is short, usually empty)
+    int32_t* const rr = kparams<StepParams<T>>().S.rerun;
+    int32_t* const done = kparams<StepParams<T>>().S.rdone;
+    if (!done) {  // serial: the 64-contact launch has ended
+      const int n = rr[0];
+      for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
+        step_arena<T, DIM, IK>(smem, rr[1 + i] - 1);
+        FULL_SYNC();
+      }
+    } else {
+      // concurrent: slot i is taken as soon as it is published; the wave ends when the 64-contact launch has ended
+      // and published no slot i (and, as a guard that every wave reaches, after 20 s of waiting)
+      const int nwg = kparams<StepParams<T>>().S.rdone_of;
+      const unsigned long long t_start = wall_clock64();
+      // The polls are relaxed device-scope loads (coherent reads, no cache maintenance); the acquire fence -- an
+      // invalidation of this XCD's L2, which the 64-contact waves sharing it depend on -- runs once per arena taken
+      // and once at the end, not per poll (polling with acquire loads cost the launch 11 %, profiles/r05m_*)
+      for (int i = (int)blockIdx.x; i < nwg; i += (int)gridDim.x) {  // at most one slot per 64-contact workgroup
+        int a = 0;
+        for (;;) {
+          a = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rr + 1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          if (a) break;
+          const int nd = __builtin_amdgcn_readfirstlane(__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          if (nd >= nwg) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            const int n = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (n <= i) break;
+            continue;  // published before the launch ended: its slot store is visible now
+          }
+          if (wall_clock64() - t_start > 2000000000ull) break;  // 20 s at 100 MHz
+          __builtin_amdgcn_s_sleep(127);
+        }
+        if (!a) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the resume record / backup the slot store released
+        step_arena<T, DIM, IK>(smem, a - 1);
+        FULL_SYNC();
+      }
     }
   } else {
     // longest-processing-time-first dispatch: the host orders the arenas by their last env-step's duration, so the
@@ -6054,6 +6092,11 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
     // on which workgroup steps an arena)
     const int32_t* const order_ = kparams<StepParams<T>>().S.order;
     step_arena<T, DIM, IK>(smem, order_ ? order_[blockIdx.x] : (int)blockIdx.x);
+    int32_t* const done = kparams<StepParams<T>>().S.rdone;
+    if (done) {  // concurrent rerun: relaxed (a release here would write back this XCD's L2 per workgroup); the
+                 // publishing workgroups fenced their slot store above
+      if (LANE == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

@@ -63,10 +63,13 @@ Lay rerun_layout() {
   return FixedDims<A, K, true>::template layout<sizeof(T)>();
 }
 
+// concurrent (alongside the 64-contact launch, State::rdone): 4 workgroups wait for published arenas -- an env-step
+// above 64 contacts is rare (about one arena in 60,000) and each waiting workgroup holds a wide workspace of LDS
 template <typename T, int A, int K>
-void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik) {
+void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik, bool concurrent) {
   const int lds = FixedDims<A, K, true>::template layout<sizeof(T)>().total;
-  const dim3 grid(num_arenas < 256 ? num_arenas : 256);
+  const int cap = concurrent ? 1 : 256;
+  const dim3 grid(num_arenas < cap ? num_arenas : cap);
   if (ik)
     hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, true>), grid, dim3(WAVE), lds, stream, p);
   else
@@ -77,7 +80,7 @@ static_assert(FixedDims<FM_A, FM_K, true>::template layout<sizeof(FM_REAL)>().to
               "wide rerun workspace exceeds the CU's LDS");
 template hipError_t rerun_set_attr<FM_REAL, FM_A, FM_K>();
 template Lay rerun_layout<FM_REAL, FM_A, FM_K>();
-template void rerun_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, hipStream_t, bool);
+template void rerun_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, hipStream_t, bool, bool);
 #else
 template hipError_t fixed_set_attr<FM_REAL, FM_A, FM_K>(int);
 template void fixed_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, int, hipStream_t, bool);

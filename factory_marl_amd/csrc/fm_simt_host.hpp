@@ -192,6 +192,16 @@ FM_NO_TSAN inline X atomicOr(X* p, Y v) {
   return o;
 }
 
+// scoped atomics of the concurrent wide rerun (fixed-dims kernels only; the CPU backend runs the runtime-dims
+// kernel, which only reads State::rdone as null)
+#ifndef __HIP_MEMORY_SCOPE_AGENT
+#define __HIP_MEMORY_SCOPE_AGENT 3
+#endif
+#define __hip_atomic_load(p, order, scope) (*(p))
+#define __hip_atomic_store(p, v, order, scope) (void)(*(p) = (v))
+#define __hip_atomic_fetch_add(p, v, order, scope) atomicAdd((p), (v))
+#define __builtin_amdgcn_s_sleep(n) ((void)0)
+
 // the MFMA builtin: v_mfma_f32_16x16x4_f32 over the wave (A: lane l gives A[l % 16][l / 16]; B: B[l / 16][l % 16];
 // C / D: lane l holds rows 4 (l / 16) .. + 3 of column l % 16)
 typedef float fm_host_f32x4 __attribute__((ext_vector_type(4)));

@@ -43,7 +43,8 @@ EXPERIMENT_FLAGS = {("FM_CHOL_LDS", "1"): 1, ("FM_CHOL_LDS", "2"): 2, ("FM_SERIA
                     ("FM_NO_MIDCACHE", "1"): 8, ("FM_NO_ARROW", "1"): 16, ("FM_NO_ARROW", "2"): 32,
                     ("FM_NO_SCATTER", "1"): 64, ("FM_SERIAL_FK", "1"): 128, ("FM_TWO_PASS_SETUP", "1"): 256,
                     ("FM_FORCE_RERUN", "1"): 512, ("FM_NO_RERUN", "1"): 1024, ("FM_NO_TREEBLK", "1"): 2048,
-                    ("FM_PC_SCATTER", "1"): 4096, ("FM_TB_LDSBC", "1"): 8192, ("FM_RERUN_AT_50", "1"): 16384}
+                    ("FM_PC_SCATTER", "1"): 4096, ("FM_TB_LDSBC", "1"): 8192, ("FM_RERUN_AT_50", "1"): 16384,
+                    ("FM_CONCURRENT_RERUN", "1"): 32768}
 
 # global scalars of the handle (fm_set_param), per-arena values of the state record, fixed at creation
 RUNTIME_PARAMS = ("pt_time", "initial_conveyor_speed", "conveyor_acceleration", "force_contact_threshold",

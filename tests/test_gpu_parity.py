@@ -424,6 +424,20 @@ def test_wide_rerun_kernel_matches_oracle(trajectory, precision):
         assert np.mean(e <= 1e-4) >= 0.985 and e.max() <= 5e-4
 
 
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("resume", [False, True])
+def test_concurrent_wide_rerun_matches_oracle(trajectory, resume):
+    """the experiment FM_CONCURRENT_RERUN=1 (the wide kernel on a side stream, taking each abandoned arena as the
+    64-contact launch publishes it): every env-step abandoned at its first stage, or at substep 50 and
+    resumed there -- the serial rerun's fp64 gates, every arena stepped once by the wide kernel"""
+    exp = ("FM_RERUN_AT_50=1" if resume else "FM_FORCE_RERUN=1") + " FM_CONCURRENT_RERUN=1"
+    r = pu.compare(trajectory, "fp64", A, K, experiment=exp)
+    e = r["errs"]
+    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
+    assert int(r["counters"][:, 8].sum()) == len(trajectory[0])
+    assert e.max() <= 1e-7 and r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
+
+
 def _crowded_states(oracle, n_states, lo=66, hi=110, seed=0):
     """(2,4) records whose first stage holds lo..hi contacts: the cubes landed at their parking spots (16 floor
     contacts), then both arms set (qpos and the stage positions, at rest) to random joint poses that reach into the

@@ -47,7 +47,7 @@ def main():
     bench.preroll(env, 200, 0, env.device)
     g = torch.Generator(device=env.device)
     g.manual_seed(0)
-    costs, ms, reruns, newton = [], [], [], []
+    costs, ms, reruns, newton, contacts, objs = [], [], [], [], [], []
     for _ in range(a.steps):
         act = bench.random_actions(env, torch.rand(N, env.act_dim, device=env.device, generator=g))
         c0 = env.counters()
@@ -59,6 +59,8 @@ def main():
         d = env.counters() - c0
         reruns.append(int(d[:, 8].sum()))
         newton.append(d[:, 1].astype(np.float64))
+        contacts.append(d[:, 4].astype(np.float64))  # contacts demanded, summed over the step's stages
+        objs.append(d[:, 6].astype(np.float64))  # objects in scene at the step's end
         costs.append(env.costs().astype(np.float64) / 1e5)  # 100 MHz wall clock -> ms
     env.close()
     rows = []
@@ -70,7 +72,15 @@ def main():
                          lpt_prev_order_ms=round(makespan(np.argsort(-costs[k - 1]), cur, a.slots), 2),
                          plain_order_ms=round(makespan(np.arange(N), cur, a.slots), 2),
                          corr_prev_cost=round(float(np.corrcoef(costs[k - 1], cur)[0, 1]), 3),
-                         corr_newton_iters=round(float(np.corrcoef(newton[k], cur)[0, 1]), 3)))
+                         corr_newton_iters=round(float(np.corrcoef(newton[k], cur)[0, 1]), 3),
+                         # intrinsic-work predictors from the previous step's counters (a duration also carries the
+                         # co-scheduled wave's load): longest-first by them, and their correlation with this step's cost
+                         lpt_prev_newton_ms=round(makespan(np.argsort(-newton[k - 1]), cur, a.slots), 2),
+                         lpt_prev_contacts_ms=round(makespan(np.argsort(-contacts[k - 1]), cur, a.slots), 2),
+                         lpt_prev_objects_ms=round(makespan(np.argsort(-objs[k - 1], kind="stable"), cur, a.slots), 2),
+                         corr_contacts=round(float(np.corrcoef(contacts[k], cur)[0, 1]), 3),
+                         corr_prev_contacts=round(float(np.corrcoef(contacts[k - 1], cur)[0, 1]), 3),
+                         corr_prev_newton=round(float(np.corrcoef(newton[k - 1], cur)[0, 1]), 3)))
     rep = dict(source="tools/cost_probe.py: config-2 workload (4096 arenas (2,4) fp32, 200-step pre-roll), fm_get_costs "
                       "after each step; list-scheduling replay over %d wave slots" % a.slots, steps=rows)
     txt = json.dumps(rep, indent=1)
