@@ -13,7 +13,7 @@
 #   c3 c4 c5    config 3 / 4 (one GPU) / 5 benches             ktrace              rocprofv3 kernel trace + stats
 #   pmc         PMC passes (FETCH, WRITE, SQ, VALU) + summaries
 #   phase       phase profiles (2,4) fp32 / fp64, (2,8), (4,16)     phase24   (2,4) fp32 only
-#   pmcsq       the SQ counter pass alone (waits, LDS bank conflicts)
+#   pmcsq       the SQ counter pass alone (waits, LDS bank conflicts)      pmcic   instruction-cache counters
 #   flags       1000-episode flag-divergence study (fp32, fp64)
 set -o pipefail
 TAG=${1:?tag}
@@ -129,6 +129,12 @@ for l in open('$O/$step$S.jsonl'):
         > $O/pmc_sq$S.log 2>&1 || fail pmc_sq $? $O/pmc_sq$S.log
       python tools/pmc_sq.py $(find $O/pmc_sq$S -name "*counter_collection.csv" | head -1) $O/pmc_sq_summary$S.json \
         || fail sq $? ;;
+    pmcic)
+      timeout -s KILL 150 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE \
+        SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $O/pmc_ic$S -- python3 bench.py $P \
+        > $O/pmc_ic$S.log 2>&1 || fail pmc_ic $? $O/pmc_ic$S.log
+      python tools/pmc_sq.py $(find $O/pmc_ic$S -name "*counter_collection.csv" | head -1) $O/pmc_ic_summary$S.json \
+        || fail ic $? ;;
     phase)
       timeout -k 10 200 python tools/phase_profile.py --precision fp32 > $O/phase_fp32$S.json 2> $O/phase$S.err \
         || fail phase32 $? $O/phase$S.err

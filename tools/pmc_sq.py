@@ -10,14 +10,20 @@ from collections import defaultdict
 
 def fractions(c):
     def div(a, b):
-        return c[a] / c[b] if c[b] else None
+        return c[a] / c[b] if c.get(a) is not None and c.get(b) else None
 
     return {"wait_any_frac_of_wave_cycles": div("SQ_WAIT_ANY", "SQ_WAVE_CYCLES"),
             "wait_inst_any_frac": div("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"),
             "active_inst_frac": div("SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"),
             "lds_bank_conflict_frac_of_lds_active": div("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"),
             "lds_bank_conflict_frac_of_wave_cycles": div("SQ_LDS_BANK_CONFLICT", "SQ_WAVE_CYCLES"),
-            "valu_per_lds": div("SQ_INSTS_VALU", "SQ_INSTS_LDS")}
+            "valu_per_lds": div("SQ_INSTS_VALU", "SQ_INSTS_LDS"),
+            # the instruction-cache pass (gpu_measure.sh pmcic): the kernel's ~60k instructions against 64 KB of
+            # instruction cache per pair of CUs
+            "icache_hit_frac": div("SQC_ICACHE_HITS", "SQC_ICACHE_REQ"),
+            "icache_miss_frac": div("SQC_ICACHE_MISSES", "SQC_ICACHE_REQ"),
+            "icache_misses_per_wave_kcycle": (1000.0 * c["SQC_ICACHE_MISSES"] / c["SQ_WAVE_CYCLES"]
+                                              if c.get("SQ_WAVE_CYCLES") and "SQC_ICACHE_MISSES" in c else None)}
 
 
 def main(src, dst):
