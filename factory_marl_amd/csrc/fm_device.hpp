@@ -629,14 +629,20 @@ __device__ __forceinline__ T impedance(const T* si, T x) {
   dmin = dmin < lo ? lo : (dmin > hi ? hi : dmin);
   dmax = dmax < lo ? lo : (dmax > hi ? hi : dmax);
   if (dmin == dmax || width <= T(1e-15)) return T(0.5) * (dmin + dmax);
-  x = fabs(x) / width;
+  const T ax = fabs(x);
+  if (power == T(2)) {  // every contact class of this scene (solimp power 2): x = |d| / width folded into one division
+    if (ax >= width) return dmax;
+    if (ax <= T(0)) return dmin;
+    const T r = width - ax;
+    const T y = ax <= mid * width ? ax * ax / (width * width * mid) : T(1) - r * r / (width * width * (T(1) - mid));
+    return dmin + y * (dmax - dmin);
+  }
+  x = ax / width;
   if (x >= T(1)) return dmax;
   if (x <= T(0)) return dmin;
   T y;
   if (power == T(1))
     y = x;
-  else if (power == T(2))  // every contact class of this scene (solimp power 2): pow without the library call
-    y = x <= mid ? x * x / mid : T(1) - (T(1) - x) * (T(1) - x) / (T(1) - mid);
   else if (x <= mid)
     y = pow(x, power) / pow(mid, power - T(1));
   else
@@ -2653,10 +2659,10 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
     };
     const double tran = invw_t(kb1) + invw_t(kb2);
     const double diag = tran + mu * mu * tran;
-    double R = (1.0 - imp) * diag / imp;
-    R = R > 1e-15 ? R : 1e-15;
+    // D = 1 / max(R, 1e-15), R = (1 - imp) diag / imp: one division on the lane's chain instead of two
+    const double D = imp / ((1.0 - imp) * diag);
     cr[CR_MU] = (T)mu;
-    cr[CR_D] = (T)(1.0 / R);
+    cr[CR_D] = (T)(D < 1e15 ? D : 1e15);
     // pyramid edges: the position term of aref with K / (4 mu^2), pinned by MuJoCo's resting equilibria and
     // belt-carried velocities in the reference runs (oracle/solver.c, tests/test_physics_pins.py)
     cr[CR_KD] = (T)(Kk * imp * dist / (4.0 * mu * mu));
@@ -2720,9 +2726,8 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
         const double imp = impedance(si, pos);
         double Kk, Bb;
         kb_params(M.timestep, sr, si, Kk, Bb);
-        double R = (1.0 - imp) * (double)diag / imp;
-        R = R > 1e-15 ? R : 1e-15;
-        rr[RR_D] = (T)(1.0 / R);
+        const double D = imp / ((1.0 - imp) * (double)diag);  // 1 / max(R, 1e-15), one division
+        rr[RR_D] = (T)(D < 1e15 ? D : 1e15);
         const double* vd = w.vd();
         const double vel = (double)c0 * vd[d0] + (d1 >= 0 ? (double)c1 * vd[d1] : 0.0);
         rr[RR_AREF] = (T)(-Bb * vel - Kk * imp * pos);
@@ -4686,7 +4691,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     }
     gn = wave_sum(gn);
     PMARK(PH_NGRAD);
-    if (scale * sqrt(gn) < tol) break;
+    if (scale * scale * gn < tol * tol) break;  // scale |g| < tol without the float64 square root on the chain
     // arrowhead substeps of the (2,4) scene (no contact couples two trees other than the belt: nearly every
     // substep): H is assembled straight into the block-parallel factor's registers, no LDS Hessian
     bool solved = false;
