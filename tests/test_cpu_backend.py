@@ -88,3 +88,11 @@ def test_state_roundtrip_on_the_host(lib):
     assert np.array_equal(env.get_state(), s0)
     assert env.device == torch.device("cpu")
     env.close()
+
+
+def test_config3_scene_matches_the_oracle(lib, oracle):
+    """the (2,8) scene of configs 3 / 4 on the host: teacher-forced fp64 against the oracle"""
+    tr = pu.rollout(oracle, 2, 8, 24, seed_actions=3)
+    r = pu.compare(tr, "fp64", 2, 8, device="cpu")
+    s = pu.summary(r)
+    assert s["int_bad"] == 0 and s["flag_bad"] == 0 and s["worst"] <= 1e-7, s

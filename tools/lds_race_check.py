@@ -8,7 +8,9 @@ with the race detector (fm_cpu.cpp FM_RACE_DETECT: the TSan instrumentation hook
 over a few env-steps of each env class and prints every pair of source lines where two lanes touched the same LDS
 word between two rendezvous with at least one write (RAW / WAR / WAW), symbolized with llvm-symbolizer.
 
-usage: tools/lds_race_check.sh   (builds factory_marl_amd/lib_race.so, then runs this with FACTORYSIM_LIB set)"""
+usage: make -C factory_marl_amd/csrc race      (builds scratch/lib_race.so)
+       FACTORYSIM_LIB=scratch/lib_race.so python tools/lds_race_check.py
+       [RACE_STEPS=n] [RACE_CASES=i,j] [RACE_PRECISIONS=fp64,fp32]   (one case takes ~10 min: run cases in parallel)"""
 import ctypes as C
 import os
 import subprocess
