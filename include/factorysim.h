@@ -102,7 +102,11 @@ void fm_config_default(fm_config* cfg);
 
 /* Create N arenas on `device`.  seeds: host array [N] -- per-arena seed used, as in the reference,
  * both for build_scene's cube sizes (scene.py:121) and for the TaskManager RNG (task_utils.py:19).
- * NULL = every arena uses seed 42 (the value in every saved run config under runs/). */
+ * NULL = every arena uses seed 42 (the value in every saved run config under runs/).
+ * device = -1: the CPU backend -- the same kernels on host threads, every buffer argument of the
+ * handle's calls host memory, results identical in meaning (reference config 1: visualisation.py:32-77 steps one env
+ * on the CPU); fm_render and fm_profile return FM_EINVAL.  A GPU device that is absent is FM_EDEVICE, never a CPU
+ * fallback. */
 int fm_create(const fm_config* cfg, int device, const uint64_t* seeds, fm_handle** out);
 void fm_destroy(fm_handle* h);
 const char* fm_last_error(void);
