@@ -96,3 +96,40 @@ def test_config3_scene_matches_the_oracle(lib, oracle):
     r = pu.compare(tr, "fp64", 2, 8, device="cpu")
     s = pu.summary(r)
     assert s["int_bad"] == 0 and s["flag_bad"] == 0 and s["worst"] <= 1e-7, s
+
+
+def test_results_do_not_depend_on_the_lane_order(lib, trajectory, tmp_path):
+    """the kernel's lanes hand data to each other only at SYNC(): running each emulated wave's lanes
+    in reverse order (FACTORYSIM_CPU_REVERSE=1, read once per process: a child process) gives the same env-steps --
+    up to the summation order of the LDS float64 atomics (the J'f scatter), so within 1e-9 relative in fp64"""
+    import subprocess
+    import sys
+
+    recs, acts, _ = trajectory
+    np.savez(tmp_path / "in.npz", recs=recs[:24], acts=acts[:24])
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+sys.path.insert(0, {repr(os.path.dirname(os.path.abspath(__file__)))})
+import parity_util as pu, torch
+d = np.load({repr(str(tmp_path / "in.npz"))})
+env = pu.gpu_env(len(d["recs"]), "fp64", {A}, {K}, device="cpu")
+env.set_state(d["recs"])
+env.step_tensors(torch.as_tensor(d["acts"]))
+np.save({repr(str(tmp_path / "out.npy"))}, env.get_state())
+"""
+    env = dict(os.environ, FACTORYSIM_CPU_REVERSE="1")
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=600)
+    rev = np.load(tmp_path / "out.npy")
+    fwd_env = pu.gpu_env(24, "fp64", A, K, device="cpu")
+    fwd_env.set_state(recs[:24])
+    fwd_env.step_tensors(torch.as_tensor(acts[:24]))
+    fwd = fwd_env.get_state()
+    from factory_marl_amd import state as st
+
+    for s in range(24):
+        gd, gi, gr = st.unpack(A, K, fwd[s])
+        rd, ri, rg = st.unpack(A, K, rev[s])
+        assert np.array_equal(gi, ri) and np.array_equal(gr, rg), s
+        qd, vd = pu.state_err(A, K, rd, gd)
+        assert max(qd.max(), vd.max()) <= 1e-9, (s, qd.max(), vd.max())
