@@ -1,13 +1,16 @@
 """ctypes binding of libfactorysim.so (the C ABI in include/factorysim.h).
 
 The product path is the HIP library only: if ``libfactorysim.so`` is missing or cannot be loaded this
-module raises -- there is no CPU fallback.
+module raises -- there is no CPU fallback.  ``libfactorysim_exp.so`` is the experiment build of the same sources
+(``load(experimental=True)``): its kernels carry the A/B and test switches (FactoryVecEnv.set_experiment) that the
+product kernels are compiled without.
 """
 import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FACTORYSIM_LIB", os.path.join(_HERE, "libfactorysim.so"))
+EXP_LIB_PATH = os.environ.get("FACTORYSIM_EXP_LIB", os.path.join(_HERE, "libfactorysim_exp.so"))
 
 # env classes (include/factorysim.h FM_ENV_*)
 FM_ENV_FACTORY = 0
@@ -69,21 +72,22 @@ EXPORTED = [
     "fm_kernel_timing", "fm_get_kernel_time",
 ]
 
-_LIB = None
+_LIBS = {}
 
 
 class FactorySimError(RuntimeError):
     pass
 
 
-def load():
-    """Load the HIP library (raises if it is missing: the product has no fallback path)."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise FactorySimError(f"{LIB_PATH} not built: run `python __graft_entry__.py build` (hipcc, gfx950)")
-    L = C.CDLL(LIB_PATH)
+def load(experimental=False):
+    """Load the HIP library (raises if it is missing: the product has no fallback path); experimental: the
+    experiment build (libfactorysim_exp.so, A/B and test switches compiled in)."""
+    path = EXP_LIB_PATH if experimental else LIB_PATH
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise FactorySimError(f"{path} not built: run `python __graft_entry__.py build` (hipcc, gfx950)")
+    L = C.CDLL(path)
     P, I = C.c_void_p, C.c_int
     L.fm_config_default.argtypes = [C.POINTER(FmConfig)]
     L.fm_config_default.restype = None
@@ -133,7 +137,7 @@ def load():
     if hasattr(L, "fm_num_counters"):
         L.fm_num_counters.argtypes = []
         L.fm_num_counters.restype = I
-    _LIB = L
+    _LIBS[path] = L
     return L
 
 
@@ -142,9 +146,10 @@ def num_counters(L):
     return L.fm_num_counters() if hasattr(L, "fm_num_counters") else 8
 
 
-def check(rc):
+def check(rc, L=None):
+    """raise on a nonzero status code with the library's error text (L: the library that returned it)"""
     if rc != 0:
-        raise FactorySimError(f"factorysim error {rc}: {load().fm_last_error().decode()}")
+        raise FactorySimError(f"factorysim error {rc}: {(L or load()).fm_last_error().decode()}")
 
 
 def scene_mjcf(num_arms=2, max_num_objects=10, seed=42, meshdir=None):

@@ -22,7 +22,7 @@ hipError_t rerun_set_attr();
 template <typename T, int A, int K>
 Lay rerun_layout();
 template <typename T, int A, int K>
-void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik, bool concurrent);
+void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik);
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes);
 template <typename T, int A, int K>
@@ -34,8 +34,14 @@ void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStre
 // =================================================================================================
 using namespace fm;
 
-// the CPU backend's kernels (fm_cpu.cpp: fm_device.hpp compiled for the host, the wave emulated)
+// the CPU backend's kernels (fm_cpu.cpp: fm_device.hpp compiled for the host, the wave emulated; fm_cpu_fixed.cpp: the
+// compile-time scenes, one entry per scene -- wide = 1 the (2,4) float64 wide rerun kernel)
 extern "C" void fm_cpu_step(int fp64, const void* params, int num_arenas, int lds_bytes, int ik);
+#define X(a, k) extern "C" int fm_cpu_step_fixed_##a##_##k(int fp64, int wide, const void* params, int grid, int lds_bytes, int ik);
+FM_FIXED_SCENES
+FM_FIXED_SCENES32
+X(2, 4)  // always linked (the wide rerun kernel)
+#undef X
 extern "C" void fm_cpu_reset(int fp64, const void* model, const void* state, const void* lay, float* obs,
                              const uint8_t* mask, int num_arenas, int lds_bytes);
 extern "C" void fm_cpu_debug(int fp64, const void* model, const void* state, const void* lay, int arena, int actuated,
@@ -70,17 +76,6 @@ static int set_err(int code, const std::string& msg) {
     if (e_ != hipSuccess) return set_err(FM_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-// inside a launch sequence (void): a failed event record / wait falls back to a device-wide synchronisation, which
-// orders the two streams' work as the event would have
-#define HIPCHKV(x)                                                                                 \
-  do {                                                                                             \
-    hipError_t e_ = (x);                                                                           \
-    if (e_ != hipSuccess) {                                                                        \
-      fprintf(stderr, "factorysim: %s: %s\n", #x, hipGetErrorString(e_));                          \
-      (void)hipDeviceSynchronize();                                                                \
-    }                                                                                              \
-  } while (0)
-
 struct fm_handle {
   fm_config cfg;
   SceneHost sc;
@@ -94,26 +89,30 @@ struct fm_handle {
   bool was_reset = false;
   Lay lay;
   std::vector<void*> allocs;
-  // device model arrays (typed by precision, stored as void*)
-  void* arm_base = nullptr;
+  // device model arrays: the precision-typed ones (and the frame-dependent float64 geom table) per kernel precision
+  // -- `tab` for the handle's own kernels, `tab64` (fp32 handles of the benchmark scene) for the float64 wide rerun
+  // kernel, which steps the abandoned env-steps of both builds
+  struct Tables {
+    void* arm_base = nullptr;
+    void* body = nullptr;
+    void* dof = nullptr;
+    void* ctrlrange = nullptr;
+    void* geom = nullptr;
+    void* geomd = nullptr;  // float64, but in the kernel frame of its precision (zshift)
+    void* cbs = nullptr;
+    void* cube = nullptr;
+    void* meaninertia = nullptr;
+  } tab, tab64;
   double* ctrlrange_d = nullptr;
   double* arm_base_w = nullptr;
-  void* body = nullptr;
-  void* dof = nullptr;
   double* dofd = nullptr;
-  void* ctrlrange = nullptr;
-  void* geom = nullptr;
-  void* geomd = nullptr;
   int* geom_i = nullptr;
   int* ginfo = nullptr;
   int* cbi = nullptr;
-  void* cbs = nullptr;
   uint16_t* cbg = nullptr;
   uint32_t* cbp = nullptr;
   uint32_t* pair = nullptr;
   void* param = nullptr;
-  void* cube = nullptr;
-  void* meaninertia = nullptr;
   uint32_t* tri = nullptr;
   // state
   void* phys = nullptr;
@@ -136,14 +135,10 @@ struct fm_handle {
   int fixed = -1;  // index into FM_FIXED_SCENES, -1 = runtime-dims kernel
   Lay lay_step{};  // workspace layout of the env-step kernel in use
   bool spill = false;          // DimsSpill: Hessian + contact records in per-arena global scratch (fp64, > 160 KiB)
-  uint32_t xflags = 0;         // experiment switches (Model::dbg_flags): read once at fm_create, fm_set_param
+  uint32_t xflags = 0;         // the experiment build's switches (Model::dbg_flags): read at fm_create, fm_set_param
   // the benchmark scene's lossless contacts: [1 + N] rerun list of the 64-contact launch (fm_dev.hpp State::rerun),
-  // the IK classes' record backup, the wide kernel's layout
+  // the IK classes' record backup, the (float64) wide kernel's layout
   int32_t* rerun = nullptr;
-  // concurrent rerun: the wide kernel runs on a side stream alongside the 64-contact launch (State::rdone)
-  int32_t* rdone = nullptr;
-  hipStream_t rstream = nullptr;
-  hipEvent_t rev_start = nullptr, rev_end = nullptr;
   char* bak = nullptr;
   double* resume = nullptr;    // [N][resume_stride] substep state of an abandoned env-step
   Lay lay_rerun{};
@@ -249,62 +244,60 @@ static Model<T> make_model(const fm_handle* h) {
     M.ik_time.move_steps = (int)(1.0 / dt);
     M.ik_time.timeout_steps = (int)(3.0 / dt);
   }
-  M.arm_base = (const T*)h->arm_base;
+  // a float64 model of an fp32 handle: the float64 wide rerun kernel's tables
+  const fm_handle::Tables& t = (sizeof(T) == 8 && !h->fp64) ? h->tab64 : h->tab;
+  M.arm_base = (const T*)t.arm_base;
   M.arm_base_w = h->arm_base_w;
-  M.body = (const T*)h->body;
-  M.dof = (const T*)h->dof;
+  M.body = (const T*)t.body;
+  M.dof = (const T*)t.dof;
   M.dofd = h->dofd;
-  M.ctrlrange = (const T*)h->ctrlrange;
+  M.ctrlrange = (const T*)t.ctrlrange;
   M.ctrlrange_d = h->ctrlrange_d;
-  M.geom = (const T*)h->geom;
-  M.geomd = (const double*)h->geomd;
+  M.geom = (const T*)t.geom;
+  M.geomd = (const double*)t.geomd;
   M.geom_i = h->geom_i;
   M.pair = h->pair;
   M.ginfo = h->ginfo;
   M.cbi = h->cbi;
-  M.cbs = (const T*)h->cbs;
+  M.cbs = (const T*)t.cbs;
   M.cbg = h->cbg;
   M.cbp = h->cbp;
   for (int a = 0; a < 5; a++)
     for (int b = 0; b < 5; b++) M.ptab[5 * a + b] = h->sc.ptab[a][b];
   M.param = (const double*)h->param;
-  M.cube = (const T*)h->cube;
-  M.meaninertia = (const T*)h->meaninertia;
+  M.cube = (const T*)t.cube;
+  M.meaninertia = (const T*)t.meaninertia;
   M.tri = h->tri;
   M.prof = h->prof_on ? h->prof : nullptr;
+#if FM_EXPERIMENTS
   M.dbg_flags = h->xflags;
+#endif
   M.ovf_abort = 0;
   M.obs64 = c.obs_float64 != 0;
   return M;
 }
 
-// experiment switches of the kernel (A/B probes and the equivalence tests; every default is 0): read from the
-// environment once, at fm_create, and reported on stderr when any is set; "experiment_flags" (fm_set_param) changes
-// them on a live handle for later launches
-constexpr uint32_t FM_XFLAGS_MASK = 0xFFFFu;  // the switches below (fm_set_param rejects other bits)
+// the experiment build's switches (libfactorysim_exp.so, FM_EXPERIMENTS=1: the equivalence tests' reference forms and
+// the rerun path's test hooks; every default is 0): read from the environment once, at fm_create, and reported on
+// stderr when any is set; "experiment_flags" (fm_set_param) changes them on a live handle for later launches.  The
+// product library has none (FM_XF is 0 in its kernels; fm_set_param rejects "experiment_flags")
+constexpr uint32_t FM_XFLAGS_MASK = 2u | 4u | 8u | 16u | 512u | 1024u | 2048u | 16384u;
 static uint32_t read_experiment_flags() {
+#if FM_EXPERIMENTS
   struct Sw {
     const char* var;
     char val;
     uint32_t bit;
   };
   static const Sw sw[] = {
-      {"FM_CHOL_LDS", '1', 1},         // sparse LDS Cholesky instead of the register / matrix-core factors
-      {"FM_CHOL_LDS", '2', 2},         // (4,16): the sparse LDS Cholesky instead of the dense matrix-core one
+      {"FM_CHOL_LDS", '2', 2},         // (4,16): the sparse LDS Cholesky of the dense Hessian (no tree-block solve)
       {"FM_SERIAL_BOXBOX", '1', 4},    // one lane per box-box pair throughout
       {"FM_NO_MIDCACHE", '1', 8},      // the midphase list rebuilt at every substep
       {"FM_NO_ARROW", '1', 16},        // no block-parallel arrowhead Cholesky
-      {"FM_NO_ARROW", '2', 32},        // arrowhead factor of the LDS-assembled Hessian
-      {"FM_NO_SCATTER", '1', 64},      // per-dof gather of J' f instead of the scatter
-      {"FM_SERIAL_FK", '1', 128},      // arm kinematics / RNE on one lane per arm
-      {"FM_TWO_PASS_SETUP", '1', 256}, // the warmstart candidates in two row passes
       {"FM_FORCE_RERUN", '1', 512},    // (2,4): every env-step abandoned at its first stage and run by the wide kernel
       {"FM_NO_RERUN", '1', 1024},      // (2,4): contacts above 64 cut (counted), no wide rerun
       {"FM_NO_TREEBLK", '1', 2048},    // (2,8), (2,10), (4,16) fp32, wide rerun: the dense Hessian + factors on every substep
-      {"FM_PC_SCATTER", '1', 4096},    // (2,4): J' f by the per-contact scatter instead of per (contact, column)
-      {"FM_TB_LDSBC", '1', 8192},      // tree-block solve: its coupled system by the LDS-broadcast register factor
       {"FM_RERUN_AT_50", '1', 16384},  // (2,4): every env-step abandoned at substep 50, resumed there by the wide kernel
-      {"FM_CONCURRENT_RERUN", '1', 32768},  // (2,4): the wide kernel alongside the 64-contact launch (side stream)
   };
   uint32_t f = 0;
   for (const Sw& x : sw) {
@@ -313,6 +306,9 @@ static uint32_t read_experiment_flags() {
   }
   if (f) fprintf(stderr, "factorysim: experiment switches active (flags 0x%x)\n", f);
   return f;
+#else
+  return 0u;
+#endif
 }
 
 template <typename T>
@@ -330,15 +326,16 @@ static State<T> make_state(const fm_handle* h) {
   return S;
 }
 
-template <typename T>
-static int create_typed(fm_handle* h) {
+// the scene tables a kernel of precision U reads in its own kernel frame (zshift<U>()): arm bases, the arm template,
+// dof ranges, control ranges, geoms (U and float64), collision-body bounds, cube sizes, mean inertia
+template <typename U>
+static int upload_tables(fm_handle* h, fm_handle::Tables& t) {
   const SceneHost& s = h->sc;
-  const Dims& d = h->dm;
   std::vector<double> arm_base(12 * s.A), body(32 * ARM_NB, 0.0), dof(4 * ARM_ND, 0.0), ctrl(2 * s.nu);
   for (int i = 0; i < s.A; i++)
     for (int k = 0; k < 12; k++) arm_base[12 * i + k] = s.arm_base[i][k];
   // world -> kernel frame (zshift, fm_dev.hpp): every absolute position the kernel reads
-  const double zs = zshift<T>();
+  const double zs = zshift<U>();
   for (int i = 0; i < s.A; i++) arm_base[12 * i + 2] -= zs;
   for (int b = 0; b < ARM_NB; b++) {
     double* o = &body[32 * b];
@@ -365,9 +362,8 @@ static int create_typed(fm_handle* h) {
     ctrl[2 * u] = s.ctrlrange[u][0];
     ctrl[2 * u + 1] = s.ctrlrange[u][1];
   }
-  int ngc = (int)s.geoms.size();
-  std::vector<double> geom(16 * ngc, 0.0), param(8 * s.params.size(), 0.0);
-  std::vector<int> geom_i(4 * ngc);
+  const int ngc = (int)s.geoms.size();
+  std::vector<double> geom(16 * ngc, 0.0);
   for (int g = 0; g < ngc; g++) {
     const GeomRec& r = s.geoms[g];
     for (int k = 0; k < 3; k++) geom[16 * g + k] = r.pos[k];
@@ -375,40 +371,80 @@ static int create_typed(fm_handle* h) {
     for (int k = 0; k < 9; k++) geom[16 * g + 3 + k] = r.R[k];
     for (int k = 0; k < 3; k++) geom[16 * g + 12 + k] = r.size[k];
     geom[16 * g + 15] = r.rbound;
-    geom_i[4 * g] = r.mjid;
-    geom_i[4 * g + 1] = r.type;
-    geom_i[4 * g + 2] = r.kbody;
-    geom_i[4 * g + 3] = s.box_slot[g];
   }
   // cube bounding radius depends on the per-arena size: use the largest possible (h <= 0.05)
   for (int g = 0; g < ngc; g++)
     if (s.geoms[g].kbody >= 2 && s.geoms[g].kbody < 2 + s.K) geom[16 * g + 15] = std::sqrt(3.0) * 0.05;
+  std::vector<double> cbs(8 * s.cbodies.size(), 0.0);
+  for (size_t b = 0; b < s.cbodies.size(); b++) {
+    const CBody& c = s.cbodies[b];
+    for (int k = 0; k < 3; k++) {
+      cbs[8 * b + k] = c.c[k];
+      cbs[8 * b + 4 + k] = c.e[k];
+    }
+    cbs[8 * b + 3] = c.r;
+    if (c.flags & CB_STATIC) cbs[8 * b + 2] -= zs;
+  }
+  // slot 3: the rounding residue of the half size in this precision (0 in fp64), so the float64 narrowphase of the
+  // fp32 build reads h exactly as (double)[0] + (double)[3]
+  std::vector<double> cb = s.cube;
+  for (size_t i = 0; i < cb.size(); i += 4) cb[i + 3] = cb[i] - (double)(U)cb[i];
+  int r;
+  if ((r = upload<U>(h, &t.arm_base, arm_base))) return r;
+  if ((r = upload<U>(h, &t.body, body))) return r;
+  if ((r = upload<U>(h, &t.dof, dof))) return r;
+  if ((r = upload<U>(h, &t.ctrlrange, ctrl))) return r;
+  if ((r = upload<U>(h, &t.geom, geom))) return r;
+  if ((r = upload<double>(h, &t.geomd, geom))) return r;
+  if ((r = upload<U>(h, &t.cbs, cbs))) return r;
+  if ((r = upload<U>(h, &t.cube, cb))) return r;
+  if ((r = upload<U>(h, &t.meaninertia, s.meaninertia))) return r;
+  return 0;
+}
+
+template <typename T>
+static int create_typed(fm_handle* h) {
+  const SceneHost& s = h->sc;
+  const Dims& d = h->dm;
+  int r;
+  if ((r = upload_tables<T>(h, h->tab))) return r;
+  {
+    std::vector<double> bw(12 * s.A), dof(4 * ARM_ND, 0.0), ctrl(2 * s.nu);
+    for (int i = 0; i < s.A; i++)
+      for (int k = 0; k < 12; k++) bw[12 * i + k] = s.arm_base[i][k];
+    for (int j = 0; j < ARM_ND; j++) {
+      dof[4 * j] = s.dof_range[j][0];
+      dof[4 * j + 1] = s.dof_range[j][1];
+      dof[4 * j + 2] = s.dof_invw[j];
+    }
+    for (int u = 0; u < s.nu; u++) {
+      ctrl[2 * u] = s.ctrlrange[u][0];
+      ctrl[2 * u + 1] = s.ctrlrange[u][1];
+    }
+    if ((r = upload_raw<double>(h, &h->arm_base_w, bw))) return r;
+    if ((r = upload_raw<double>(h, &h->dofd, dof))) return r;
+    if ((r = upload_raw<double>(h, &h->ctrlrange_d, ctrl))) return r;
+  }
+  const int ngc = (int)s.geoms.size();
+  std::vector<double> param(8 * s.params.size(), 0.0);
+  std::vector<int> geom_i(4 * ngc);
+  for (int g = 0; g < ngc; g++) {
+    const GeomRec& gr = s.geoms[g];
+    geom_i[4 * g] = gr.mjid;
+    geom_i[4 * g + 1] = gr.type;
+    geom_i[4 * g + 2] = gr.kbody;
+    geom_i[4 * g + 3] = s.box_slot[g];
+  }
   for (size_t p = 0; p < s.params.size(); p++) {
     param[8 * p] = s.params[p].mu;
     param[8 * p + 1] = s.params[p].solref[0];
     param[8 * p + 2] = s.params[p].solref[1];
     for (int k = 0; k < 5; k++) param[8 * p + 3 + k] = s.params[p].solimp[k];
   }
-  int r;
-  if ((r = upload<T>(h, &h->arm_base, arm_base))) return r;
-  {
-    std::vector<double> bw(12 * s.A);
-    for (int i = 0; i < s.A; i++)
-      for (int k = 0; k < 12; k++) bw[12 * i + k] = s.arm_base[i][k];
-    if ((r = upload_raw<double>(h, &h->arm_base_w, bw))) return r;
-  }
-  if ((r = upload<T>(h, &h->body, body))) return r;
-  if ((r = upload<T>(h, &h->dof, dof))) return r;
-  if ((r = upload_raw<double>(h, &h->dofd, dof))) return r;
-  if ((r = upload<T>(h, &h->ctrlrange, ctrl))) return r;
-  if ((r = upload_raw<double>(h, &h->ctrlrange_d, ctrl))) return r;
-  if ((r = upload<T>(h, &h->geom, geom))) return r;
-  if ((r = upload<double>(h, &h->geomd, geom))) return r;
   if ((r = upload_raw<int>(h, &h->geom_i, geom_i))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->pair, s.pairs))) return r;
   {
     std::vector<int> gin(ngc), cbi(4 * s.cbodies.size());
-    std::vector<double> cbs(8 * s.cbodies.size(), 0.0);
     for (int g = 0; g < ngc; g++) {
       const GeomRec& G = s.geoms[g];
       int tc = G.type == GT_PLANE ? GC_PLANE : (G.type == GT_SPHERE ? GC_SPHERE : GC_BOX);
@@ -421,28 +457,13 @@ static int create_typed(fm_handle* h) {
       cbi[4 * b + 1] = c.flags;
       cbi[4 * b + 2] = c.g0;
       cbi[4 * b + 3] = c.ng;
-      for (int k = 0; k < 3; k++) {
-        cbs[8 * b + k] = c.c[k];
-        cbs[8 * b + 4 + k] = c.e[k];
-      }
-      cbs[8 * b + 3] = c.r;
-      if (c.flags & CB_STATIC) cbs[8 * b + 2] -= zs;
     }
     if ((r = upload_raw<int>(h, &h->ginfo, gin))) return r;
     if ((r = upload_raw<int>(h, &h->cbi, cbi))) return r;
-    if ((r = upload<T>(h, &h->cbs, cbs))) return r;
     if ((r = upload_raw<uint16_t>(h, &h->cbg, s.cb_geoms))) return r;
     if ((r = upload_raw<uint32_t>(h, &h->cbp, s.cb_pairs))) return r;
   }
   if ((r = upload<double>(h, &h->param, param))) return r;
-  {
-    // slot 3: the rounding residue of the half size in this build's precision (0 in fp64), so the float64
-    // narrowphase of the fp32 build reads h exactly as (double)[0] + (double)[3]
-    std::vector<double> cb = s.cube;
-    for (size_t i = 0; i < cb.size(); i += 4) cb[i + 3] = cb[i] - (double)(T)cb[i];
-    if ((r = upload<T>(h, &h->cube, cb))) return r;
-  }
-  if ((r = upload<T>(h, &h->meaninertia, s.meaninertia))) return r;
   if ((r = upload_raw<uint32_t>(h, &h->tri, s.tri))) return r;
   // state
   size_t N = d.N;
@@ -482,14 +503,10 @@ static int create_typed(fm_handle* h) {
     h->allocs.push_back(h->order);
   }
   h->lay = lds_layout(d, sizeof(T));
-  if (h->cpu) {
-    // CPU backend: the runtime-dims kernel with its whole workspace in the emulated wave's host "LDS" (no 160 KiB
-    // limit, no spill layout, no compile-time scenes, no dispatch order)
-    h->lay_step = h->lay;
-    h->fixed = -1;
-    return 0;
-  }
-  if (h->lay.total > 160 * 1024) {
+  // CPU backend: the compile-time scenes run their own kernels as on the GPU (fm_cpu_fixed.cpp: spill layouts, the
+  // (2,4) wide rerun); other scenes the runtime-dims kernel with its whole workspace in the emulated wave's host "LDS"
+  // (no 160 KiB limit, no DimsSpill layout); no dispatch order
+  if (h->lay.total > 160 * 1024 && !h->cpu) {
     if constexpr (sizeof(T) == 8) {
       // fp64 scenes beyond the CU's LDS (4 arms): the parity-grade spill layout (DimsSpill, fm_dev.hpp)
       h->lay = lds_layout(d, sizeof(T), true);
@@ -510,8 +527,9 @@ static int create_typed(fm_handle* h) {
       return set_err(FM_EINVAL, "arena workspace exceeds 160 KiB of LDS");
     }
   }
-  HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             h->lay.total));
+  if (!h->cpu)
+    HIPCHK(hipFuncSetAttribute((const void*)reset_kernel<T, Dims>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               h->lay.total));
   // env-step kernel: a compile-time specialisation when the scene is one of FM_FIXED_SCENES
   h->fixed = -1;
   const char* force_dyn = getenv("FM_FORCE_DYNAMIC");
@@ -520,7 +538,7 @@ static int create_typed(fm_handle* h) {
   if (h->fixed < 0 && !(force_dyn && force_dyn[0] == '1') && FixedDims<a, k>::matches(d)) {             \
     h->fixed = idx;                                                                                      \
     h->lay_step = FixedDims<a, k>::template layout<sizeof(T)>();                                         \
-    HIPCHK((fixed_set_attr<T, a, k>(h->lay_step.total)));                                                  \
+    if (!h->cpu) HIPCHK((fixed_set_attr<T, a, k>(h->lay_step.total)));                                    \
   }                                                                                                      \
   idx++;
   FM_FIXED_SCENES
@@ -530,7 +548,7 @@ static int create_typed(fm_handle* h) {
   if (h->fixed < 0 && !(force_dyn && force_dyn[0] == '1') && FixedDims<a, k>::matches(d)) {             \
     h->fixed = idx;                                                                                      \
     h->lay_step = FixedDims<a, k>::template layout<sizeof(T)>();                                         \
-    HIPCHK((fixed_set_attr<T, a, k>(h->lay_step.total)));                                                  \
+    if (!h->cpu) HIPCHK((fixed_set_attr<T, a, k>(h->lay_step.total)));                                    \
   }                                                                                                      \
   idx++;
     FM_FIXED_SCENES32
@@ -543,17 +561,19 @@ static int create_typed(fm_handle* h) {
     h->allocs.push_back(h->spill_buf);
   }
   // the benchmark scene at its 64-contact capacity: an env-step with a stage above it is rerun by the wide kernel
+  // The wide kernel runs in float64 for both builds (an abandoned env-step is rare -- about one arena in 60,000 --
+  // and its 65-128 stiff contacts, arms pressed into the table, belt and each other with the gripper plates' small
+  // masses among them, are where a float32 Hessian misses the SURVEY gate: round 5 measured 2.7e-2 on such states);
+  // fp32 handles upload the float64 tables it reads
   if (h->fixed >= 0 && FixedDims<2, 4>::matches(d) && d.maxcon == MAXCON) {
-    HIPCHK((rerun_set_attr<T, 2, 4>()));
-    h->lay_rerun = rerun_layout<T, 2, 4>();
+    if constexpr (sizeof(T) == 4) {
+      if ((r = upload_tables<double>(h, h->tab64))) return r;
+    }
+    if (!h->cpu) HIPCHK((rerun_set_attr<double, 2, 4>()));
+    h->lay_rerun = rerun_layout<double, 2, 4>();
     HIPCHK(d_malloc(h, (void**)&h->rerun, (N + 1) * sizeof(int32_t)));
     h->allocs.push_back(h->rerun);
     HIPCHK(d_memset(h, h->rerun, 0, (N + 1) * sizeof(int32_t)));
-    HIPCHK(d_malloc(h, (void**)&h->rdone, sizeof(int32_t)));
-    h->allocs.push_back(h->rdone);
-    HIPCHK(hipStreamCreateWithFlags(&h->rstream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&h->rev_start, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&h->rev_end, hipEventDisableTiming));
     // the substep state of an abandoned env-step (the wide kernel resumes from it, fm_dev.hpp State::resume)
     HIPCHK(d_malloc(h, (void**)&h->resume, N * (size_t)resume_stride(d.nq, d.nv, d.nu) * sizeof(double)));
     h->allocs.push_back(h->resume);
@@ -565,10 +585,12 @@ static int create_typed(fm_handle* h) {
   }
   if (h->fixed < 0) {
     h->lay_step = h->lay;
-    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               h->lay.total));
-    HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               h->lay.total));
+    if (!h->cpu) {
+      HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 h->lay.total));
+      HIPCHK(hipFuncSetAttribute((const void*)step_kernel<T, Dims, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 h->lay.total));
+    }
   }
   return 0;
 }
@@ -666,20 +688,16 @@ __global__ void __launch_bounds__(1024) lpt_order_kernel(const uint32_t* __restr
   for (int i = t; i < n; i += (int)blockDim.x) order[atomicAdd(&hist[bucket(i)], 1u)] = i;
 }
 
-// the wide-capacity rerun of the arenas the 64-contact launch abandoned (one workgroup per arena of the handle;
-// the ones past the list's count exit at once)
-template <typename T>
-static void launch_rerun(fm_handle* h, const StepParams<T>& pd, bool ik, hipStream_t stream, bool concurrent) {
-  StepParams<T> pr = pd;
-  pr.L = h->lay_rerun;
+// the wide-capacity rerun of the arenas the 64-contact launch abandoned, after it on the same stream: the float64
+// kernel for both builds (a small grid; the workgroups past the list's count exit at once)
+static void launch_rerun(fm_handle* h, const StepIO& io, bool ik) {
+  StepParams<double> pr{make_model<double>(h), make_state<double>(h), h->lay_rerun, io};
   pr.S.order = nullptr;
   pr.S.rerun = h->rerun;
   pr.S.bak = h->bak;
   pr.S.resume = h->resume;
-  pr.S.rdone = concurrent ? h->rdone : nullptr;
-  pr.S.rdone_of = h->dm.N;
   pr.M.dm.maxcon = MAXCON_WIDE;  // the wide kernel keeps up to 128 contacts per stage
-  rerun_launch<T, 2, 4>(pr, h->dm.N, stream, ik, concurrent);
+  rerun_launch<double, 2, 4>(pr, h->dm.N, h->stream, ik);
 }
 
 // kernel-only timing (fm_kernel_timing): a HIP event pair on the handle's stream around each env-step kernel launch
@@ -702,20 +720,55 @@ static void ktime_clear(fm_handle* h) {
   h->ktime.clear();
 }
 
+// the CPU backend's env-step: the scene's compile-time kernel (and the (2,4) wide rerun after it) as on the GPU, or
+// the runtime-dims kernel
+template <typename T>
+static void launch_step_cpu(fm_handle* h, const StepIO& io) {
+  const bool ik = h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS;
+  const int fp64 = sizeof(T) == 8;
+  StepParams<T> pf{make_model<T>(h), make_state<T>(h), h->lay_step, io};
+  if (h->fixed < 0) {
+    cpu_step<T>(pf, h->dm.N, h->lay.total, ik);
+    return;
+  }
+  const bool rerun = h->rerun && !(h->xflags & 1024);
+  if (rerun) {
+    std::memset(h->rerun, 0, (h->dm.N + 1) * sizeof(int32_t));
+    pf.M.ovf_abort = 1;
+    pf.S.rerun = h->rerun;
+    pf.S.bak = h->bak;
+    pf.S.resume = h->resume;
+  }
+  int idx = 0;
+#define X(a, k)                                                                                      \
+  if (h->fixed == idx) (void)fm_cpu_step_fixed_##a##_##k(fp64, 0, &pf, h->dm.N, h->lay_step.total, ik); \
+  idx++;
+  FM_FIXED_SCENES
+  if constexpr (sizeof(T) == 4) {
+    FM_FIXED_SCENES32
+  }
+#undef X
+  (void)idx;
+  if (rerun) {
+    StepParams<double> pr{make_model<double>(h), make_state<double>(h), h->lay_rerun, io};
+    pr.S.order = nullptr;
+    pr.S.rerun = h->rerun;
+    pr.S.bak = h->bak;
+    pr.S.resume = h->resume;
+    pr.M.dm.maxcon = MAXCON_WIDE;
+    (void)fm_cpu_step_fixed_2_4(1, 1, &pr, h->dm.N < 256 ? h->dm.N : 256, h->lay_rerun.total, ik);
+  }
+}
+
 template <typename T>
 static void launch_step(fm_handle* h, const StepIO& io) {
   if (h->cpu) {
-    const StepParams<T> pc{make_model<T>(h), make_state<T>(h), h->lay, io};
-    cpu_step<T>(pc, h->dm.N, h->lay.total, h->cfg.env_class != FM_ENV_ALLFULLRL_PROGRESS);
+    launch_step_cpu<T>(h, io);
     return;
   }
   if (h->order) hipLaunchKernelGGL(lpt_order_kernel, dim3(1), dim3(1024), 0, h->stream, h->cost, h->order, h->dm.N);
   bool rerun = h->rerun && !(h->xflags & 1024);
-  // FM_CONCURRENT_RERUN=1: the wide kernel waits on a side stream and takes each abandoned arena as it is published
-  // (measured 9 % slower than the serial rerun -- any resident second kernel slowed the launch)
-  const bool concurrent = rerun && h->rstream && (h->xflags & 32768);
-  if (rerun && (hipMemsetAsync(h->rerun, 0, (h->dm.N + 1) * sizeof(int32_t), h->stream) != hipSuccess ||
-                (concurrent && hipMemsetAsync(h->rdone, 0, sizeof(int32_t), h->stream) != hipSuccess))) {
+  if (rerun && hipMemsetAsync(h->rerun, 0, (h->dm.N + 1) * sizeof(int32_t), h->stream) != hipSuccess) {
     // a stale list would make the rerun kernel re-step the previous launch's abandoned arenas: run without the
     // rerun list instead (stages above 64 contacts are then cut and counted in counters[0])
     fprintf(stderr, "factorysim: clearing the rerun list failed; this launch cuts contacts above 64\n");
@@ -735,24 +788,10 @@ static void launch_step(fm_handle* h, const StepIO& io) {
       pf.S.bak = h->bak;                                                                               \
       pf.S.resume = h->resume;                                                                         \
     }                                                                                                  \
-    if (concurrent) {                                                                                  \
-      /* the wide kernel on the side stream, queued before the 64-contact launch; the handle's stream \
-         waits for it before the next work */                                                          \
-      pf.S.rdone = h->rdone;                                                                           \
-      pf.S.rdone_of = h->dm.N;                                                                         \
-      HIPCHKV(hipEventRecord(h->rev_start, h->stream));                                                \
-      HIPCHKV(hipStreamWaitEvent(h->rstream, h->rev_start, 0));                                        \
-      launch_rerun<T>(h, pd, ik, h->rstream, true);                                                    \
-    }                                                                                                  \
     ktime_begin(h);                                                                                    \
     fixed_launch<T, a, k>(pf, h->dm.N, h->lay_step.total, h->stream, ik);                              \
     ktime_end(h);                                                                                      \
-    if (concurrent) {                                                                                  \
-      HIPCHKV(hipEventRecord(h->rev_end, h->rstream));                                                 \
-      HIPCHKV(hipStreamWaitEvent(h->stream, h->rev_end, 0));                                           \
-    } else if (rerun) {                                                                                \
-      launch_rerun<T>(h, pd, ik, h->stream, false);                                                    \
-    }                                                                                                  \
+    if (rerun) launch_rerun(h, io, ik);                                                                \
     return;                                                                                            \
   }                                                                                                    \
   idx++;
@@ -966,12 +1005,6 @@ void fm_destroy(fm_handle* h) {
   if (h->render_arenas_host) (void)hipHostFree(h->render_arenas_host);
   if (h->render_copied) (void)hipEventDestroy(h->render_copied);
   if (h->handoff) (void)hipEventDestroy(h->handoff);
-  if (h->rstream) {
-    (void)hipStreamSynchronize(h->rstream);
-    (void)hipStreamDestroy(h->rstream);
-  }
-  if (h->rev_start) (void)hipEventDestroy(h->rev_start);
-  if (h->rev_end) (void)hipEventDestroy(h->rev_end);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);  // never a stream the caller handed in
   delete h;
 }
@@ -1016,10 +1049,15 @@ static double* param_slot(fm_handle* h, const char* name, double* scale) {
 int fm_set_param(fm_handle* h, const char* name, double value) {
   if (!h) return set_err(FM_EINVAL, "null handle");
   if (name && std::string(name) == "experiment_flags") {
+#if FM_EXPERIMENTS
     if (!(value >= 0 && value < 65536 && value == (double)(uint32_t)value) || ((uint32_t)value & ~FM_XFLAGS_MASK))
-      return set_err(FM_EINVAL, "bad flags: experiment switches are the bits of 0x7FFF (fm_api.hip read_experiment_flags)");
+      return set_err(FM_EINVAL, "bad flags: the experiment switches are the bits of 0x4E1E (fm_api.hip read_experiment_flags)");
     h->xflags = (uint32_t)value;
     return FM_OK;
+#else
+    if (value == 0.0) return FM_OK;
+    return set_err(FM_EINVAL, "experiment switches are compiled out of the product library (libfactorysim_exp.so has them)");
+#endif
   }
   double scale;
   double* p = param_slot(h, name, &scale);

@@ -341,6 +341,10 @@ static void launch(unsigned grid, size_t lds_bytes, const void* kernarg, F&& bod
   }
 }
 
+void launch_kernel(unsigned grid, size_t lds_bytes, const void* kernarg, void (*body)(const void*)) {
+  launch(grid, lds_bytes, kernarg, [=]() { body(kernarg); });
+}
+
 }  // namespace fm_simt
 
 #ifdef FM_RACE_DETECT
@@ -593,13 +597,18 @@ static void cpu_debug(const Model<T>& M, const State<T>& S, const Lay& L, int ar
 }  // namespace fm
 
 // entry points for fm_api.hip (the parameter blocks are the same structs, laid out from the same fm_dev.hpp)
-extern "C" void fm_cpu_step(int fp64, const void* params, int num_arenas, int lds_bytes, int ik) {
+// the LDS layout of a step launch (tools/lds_race_check.py maps the racing offsets to its arrays; also called by the
+// compile-time scene objects, fm_cpu_fixed.cpp)
+extern "C" void fm_cpu_note_layout(const void* lay) {
 #ifdef FM_RACE_DETECT
-  {  // the LDS layout of the launch (tools/lds_race_check.py maps the racing offsets to its arrays)
-    const fm::Lay& L = fp64 ? ((const fm::StepParams<double>*)params)->L : ((const fm::StepParams<float>*)params)->L;
-    std::memcpy(fm_race::g_lay, &L, sizeof(fm::Lay));
-  }
+  std::memcpy(fm_race::g_lay, lay, sizeof(fm::Lay));
+#else
+  (void)lay;
 #endif
+}
+extern "C" void fm_cpu_step(int fp64, const void* params, int num_arenas, int lds_bytes, int ik) {
+  fm_cpu_note_layout(fp64 ? (const void*)&((const fm::StepParams<double>*)params)->L
+                          : (const void*)&((const fm::StepParams<float>*)params)->L);
   if (fp64)
     fm::cpu_step<double>(*(const fm::StepParams<double>*)params, num_arenas, lds_bytes, ik != 0);
   else

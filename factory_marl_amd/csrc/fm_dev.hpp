@@ -104,6 +104,19 @@ struct IkTiming {
   int release_wait, grasp_wait, move_steps, timeout_steps;
 };
 
+// The experiment build (libfactorysim_exp.so, -DFM_EXPERIMENTS=1) carries a few runtime switches: the reference forms
+// of the kernel's exact reformulations (the equivalence tests) and the rerun path's test hooks.  The product library
+// is compiled without them: FM_XF(M) is the constant 0 there, so every switch branch folds away and Model has no
+// dbg_flags field (tests/test_build_flags.py)
+#ifndef FM_EXPERIMENTS
+#define FM_EXPERIMENTS 0
+#endif
+#if FM_EXPERIMENTS
+#define FM_XF(M) ((M).dbg_flags)
+#else
+#define FM_XF(M) 0
+#endif
+
 template <typename T>
 struct Model {
   Dims dm;
@@ -143,14 +156,9 @@ struct Model {
   cptr<T> meaninertia;  // [N]
   cptr<uint32_t> tri;   // [nv (nv+1) / 2]  column-major lower triangle: i | j << 16
   unsigned long long* prof;  // [16] phase clocks (fm_profile), NULL when profiling is off
-  int dbg_flags;             // diagnostics: bit 0 = dense LDS Cholesky (FM_CHOL_LDS=1); bit 1 = the sparse LDS one
-                             // instead of the dense matrix-core one for runtime-dims fp32 (FM_CHOL_LDS=2); bit 2 = the
-                             // serial box-box narrowphase (FM_SERIAL_BOXBOX=1); bit 3 = no midphase reuse
-                             // (FM_NO_MIDCACHE=1); bit 4 = no arrowhead Cholesky (FM_NO_ARROW=1); bit 5 = the
-                             // arrowhead factor of the LDS-assembled Hessian (FM_NO_ARROW=2); bit 6 = the per-dof
-                             // gather of J' f instead of the scatter (FM_NO_SCATTER=1); bit 7 = the serial arm
-                             // kinematics (FM_SERIAL_FK=1); bit 8 = the Newton warmstart's two row passes
-                             // (FM_TWO_PASS_SETUP=1)
+#if FM_EXPERIMENTS
+  int dbg_flags;  // the experiment build's switches (fm_api.hip read_experiment_flags; FM_XF)
+#endif
   int ovf_abort;             // 1: a stage above the contact capacity abandons the env-step (State::rerun), not cut it
   int obs64;                 // 1: observation rows (obs, terminal_obs) are float64 (fm_config.obs_float64)
 };
@@ -172,12 +180,6 @@ struct State {
   // (2,4) contact overflow: [0] = count, [1 + i] = 1 + the arena ids whose env-step the 64-contact kernel abandoned
   // (0: slot not yet written) for the wide rerun kernel.  Null: the capacity cut (counted in counters[0]) instead
   gptr<int32_t> rerun{nullptr};
-  // concurrent rerun: the 64-contact launch's finished workgroups (each adds 1 after its arena, abandoned or not).
-  // The wide kernel, launched on a second stream alongside, takes each abandoned arena as soon as it is published and
-  // ends once all `rdone_of` workgroups are done and every published slot is taken (FM_CONCURRENT_RERUN=1, an
-  // experiment).  Null: the wide kernel runs after the launch (the default, serial rerun)
-  gptr<int32_t> rdone{nullptr};
-  int rdone_of{0};
   // IK classes with `rerun`: the arena's task records (dbl, ints) as the env-step found them, restored by the rerun
   // (the IK compose writes the FSM and the toggles' last actions before the substeps)
   gptr<char> bak{nullptr};
@@ -190,8 +192,8 @@ struct State {
 // doubles per arena of State::resume
 __host__ __device__ constexpr int resume_stride(int nq, int nv, int nu) { return 3 + nq + 2 * nv + 2 * nu; }
 
-// the arena's global scratch block (nullptr unless the kernel runs a DimsSpill layout; the (2,4) wide rerun kernel
-// keeps its workspace in LDS, so it never touches the 64-contact launch's blocks while running alongside it)
+// the arena's global scratch block (nullptr unless the kernel runs a spill layout; the (2,4) wide rerun kernel keeps its
+// workspace in LDS)
 template <typename DIM, typename T>
 __device__ __forceinline__ char* spill_base(const State<T>& S, int arena) {
   static_assert(!(DIM::spill && DIM::rerun), "a spilled wide rerun kernel would need scratch blocks of its own");

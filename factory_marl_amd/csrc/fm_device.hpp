@@ -1549,7 +1549,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   T infl = T(0);
   if constexpr (DIM::midcache) {
     bool moved = false;
-    const int ok = misc[MISC_MC_OK] && !(M.dbg_flags & 8);  // FM_NO_MIDCACHE=1: rebuild every substep
+    const int ok = misc[MISC_MC_OK] && !(FM_XF(M) & 8);  // FM_NO_MIDCACHE=1: rebuild every substep
     for (int b = LANE; b < dm.ncb; b += WAVE) {
       const T* o = w.cbw() + 8 * b;
       const T* p0 = w.mpos() + 3 * b;
@@ -1719,7 +1719,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   if (nsurv > 0) narrow_batch(M, w, gs, nsurv);
   NPMARK(PH_CHPANEL);
   if (nbb > 0) {
-    if (nbb <= 8 && !(M.dbg_flags & 4))
+    if (nbb <= 8 && !(FM_XF(M) & 4))  // FM_SERIAL_BOXBOX=1: one lane per pair throughout
       narrow_bb_parallel(M, w, gsb, nbb);
     else
       narrow_batch(M, w, gsb, nbb);
@@ -2410,9 +2410,9 @@ __device__ __forceinline__ void stage(const Model<T>& M, const Ws<T, DIM>& w, in
   const int A = dm.A, K = dm.K, nv = dm.nv;
   T* q = w.q();
   T* v = w.v();
-  // ---- kinematics + RNE: scans over each arm's chain (arm_fk_scan, A <= 4; FM_SERIAL_FK=1: one lane per arm),
-  // cubes (one lane per cube)
-  const bool fk_scan = dm.A <= 4 && !(M.dbg_flags & 128);
+  // ---- kinematics + RNE: scans over each arm's chain (arm_fk_scan, A <= 4; more arms: one lane per arm), cubes (one
+  // lane per cube)
+  const bool fk_scan = dm.A <= 4;
   if (fk_scan) {
     arm_fk_scan(M, w);
   } else {
@@ -2927,7 +2927,7 @@ __device__ constexpr bool arrow_scene() {
 // arrowhead test: no contact shared by two trees other than the belt (tree 0); uniform, a scalar branch
 template <typename T, typename DIM>
 __device__ __forceinline__ bool arrow_substep(const Model<T>& M, const Ws<T, DIM>& w) {
-  if (M.dbg_flags & 16) return false;
+  if (FM_XF(M) & 16) return false;  // FM_NO_ARROW=1: the general factors
   uint64_t both = 0;
 #pragma unroll
   for (int h = 0; h < DIM::MAXC / WAVE; h++) {  // tree-mask words (contacts 64 h .. 64 h + 63)
@@ -4143,20 +4143,6 @@ __device__ __forceinline__ void rows_eval2(const Model<T>& M, const Ws<T, DIM>& 
   }
 }
 
-// evaluate rows at x: contacts CR_JA = B x, generic RR_JAR = J x - aref; returns sum of 1/2 D jar^2 (active)
-template <typename T, typename DIM, typename X>
-__device__ __forceinline__ double rows_eval(const Model<T>& M, const Ws<T, DIM>& w, const X* x, int ncon, int nrow) {
-  contact_jx<double>(M, w, x, ncon, CR_JA);
-  for (int r = LANE; r < nrow; r += WAVE) {
-    const int* ri = w.ri() + 4 * r;
-    T* rr = w.rr() + RR_N * r;
-    *dslot(rr, RR_JAR) = (double)rr[RR_C0] * (double)x[ri[0]] +
-                         (ri[1] >= 0 ? (double)rr[RR_C1] * (double)x[ri[1]] : 0.0) - (double)rr[RR_AREF];
-  }
-  SYNC();
-  return rows_cost(w, ncon, nrow);
-}
-
 // f3 (per contact, float64 in CR_F3) = D * sum_active jar_e c_e, the frame force of the gradient; the edge forces
 // -D jar_e (active edges) in CR_F
 template <typename T, typename DIM>
@@ -4293,7 +4279,7 @@ __device__ __forceinline__ void gather_JtF_sc(const Model<T>& M, const Ws<T, DIM
 //  * the rest -- the coupled trees (an arm grasping a cube, two cubes touching: 15-24 dofs measured on the oracle's
 //    PauseIKToggle trajectories) plus the belt, with the singles' Schur terms sum l_t'l_t and sum l_t'y_t folded into
 //    the belt's diagonal and right-hand side -- is one small dense system for the register Cholesky
-//    (chol_solve_rl<TB_MAXR>: pivots by v_readlane; FM_TB_LDSBC=1 the LDS-broadcast chol_solve_reg);
+//    (chol_solve_rl<TB_MAXR>: pivots by v_readlane; the LDS-broadcast chol_solve_reg measured 4.6 % slower);
 //  * the singles' backward solves take the belt's solution from it.
 // The blocks are assembled in LDS (the Newton phase's share of the collision scratch): one lane per contact adds
 // B_a'K B_a, B_b'K B_b and the cross term B_a'K B_b (a belt row, the coupled system, or -- a contact inside one
@@ -4571,10 +4557,7 @@ __device__ __forceinline__ bool newton_treeblk(const Model<T>& M, const Ws<T, DI
   for (int i = LANE; i < n; i += WAVE)
     grest[i] = i < m ? g[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] : g[0] + (double)LY;
   SYNC();
-  if (M.dbg_flags & 8192)
-    chol_solve_reg<T, TB_MAXR>(R, w.bc(), n, grest, xr);
-  else
-    chol_solve_rl<TB_MAXR, T>(R, n, grest, xr);
+  chol_solve_rl<TB_MAXR, T>(R, n, grest, xr);
   // ---- back substitution: the coupled positions and the belt from the dense solve, the singles on their lanes
   const T xb = xr[m];
   for (int i = LANE; i < m; i += WAVE) dir[tree_dof(dm, cmap[i] >> 4) + (cmap[i] & 15)] = xr[i];
@@ -4625,7 +4608,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   // quadratic part is zero), so in the common case (the warmstart wins) the row products and M(a - as) left
   // behind are already those of the chosen start and need no third evaluation
   double qc, cost;
-  if (!(M.dbg_flags & 256)) {
+  {
     // both candidates' row products in one pass (rows_eval2); the smooth candidate's land in the JD slots
     rows_eval2(M, w, as, a, ncon, nrow);
     SYNC();
@@ -4651,34 +4634,20 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       cost = qc + c_sm;
       SYNC();
     }
-  } else {
-    const double c_sm = rows_eval(M, w, as, ncon, nrow);
-    SYNC();
-    SPLITMARK(1, PH_CHSOLVE);
-    qc = quad(a);
-    cost = qc + rows_eval(M, w, a, ncon, nrow);
-    SYNC();
-    if (!(cost < c_sm)) {
-      for (int i = LANE; i < nv; i += WAVE) a[i] = (double)as[i];
-      SYNC();
-      qc = quad(a);
-      cost = qc + rows_eval(M, w, a, ncon, nrow);
-      SYNC();
-    }
   }
   PMARK(PH_NSETUP);
   int it;
   const int maxit = M.solver_iter;
-  const bool scatter = arrow_scene<T, DIM>() && !(M.dbg_flags & 64);  // gather_JtF_sc (FM_NO_SCATTER=1: off)
+  constexpr bool scatter = arrow_scene<T, DIM>();  // gather_JtF_sc
   const int ntri = nv * (nv + 1) / 2;
   for (it = 0; it < maxit; it++) {
     // gradient g = M(a - as) + J' D jar (active)
     contact_f3(w, ncon);
     SYNC();
     SPLITMARK(2, PH_CHDIAG);
-    if (scatter && !(M.dbg_flags & 4096))
+    if constexpr (scatter)
       gather_JtF_sc(M, w, ncon, nrow, g, tmp);
-    else if ((pc_scene<T, DIM>() || scatter) && !(M.dbg_flags & 64))
+    else if constexpr (pc_scene<T, DIM>())
       gather_JtF_pc(M, w, ncon, nrow, g, tmp);
     else
       gather_JtF(M, w, ncon, nrow, g, false);
@@ -4696,7 +4665,7 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     // substep): H is assembled straight into the block-parallel factor's registers, no LDS Hessian
     bool solved = false;
     if constexpr (arrow_scene<T, DIM>()) {
-      if (!(M.dbg_flags & 32) && arrow_substep(M, w)) {
+      if (arrow_substep(M, w)) {
         contact_K(w, ncon);
         SYNC();
         chol_arrow_rl<T, DIM, true>(M, w, H, g, dir, ncon, nrow);
@@ -4705,7 +4674,8 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
       }
     }
     if constexpr (treeblk_scene<T, DIM>()) {
-      if (!solved && !(M.dbg_flags & (2048 | 3)) && newton_treeblk<T, DIM>(M, w, g, dir, ncon, nrow)) {
+      // FM_NO_TREEBLK=1 / FM_CHOL_LDS=2: the dense Hessian and its factors (the equivalence tests' reference forms)
+      if (!solved && !(FM_XF(M) & (2048 | 2)) && newton_treeblk<T, DIM>(M, w, g, dir, ncon, nrow)) {
         PMARK(PH_NCHOL);
         solved = true;
       }
@@ -4790,16 +4760,16 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
     }
     SYNC();
     PMARK(PH_NHESS);
-    if (nv <= 48 && !(M.dbg_flags & 1)) {
+    if (nv <= 48) {
       if constexpr (DIM::fixed && DIM::MAXC == WAVE)  // tree masks of one word
         chol_sparse_rl<T, DIM>(M, w, H, g, dir);
       else
         chol_solve_reg<T, 48>(H, w.bc(), nv, g, dir);
       PMARK(PH_NCHOL);
-    } else if (nv <= 64 && !(M.dbg_flags & 1)) {
+    } else if (nv <= 64) {
       chol_solve_reg<T, 64>(H, w.bc(), nv, g, dir);
       PMARK(PH_NCHOL);
-    } else if (border_chol<T, DIM>() && !(M.dbg_flags & 1)) {
+    } else if (border_chol<T, DIM>()) {
       if constexpr (border_chol<T, DIM>()) {
         if (arrow_substep(M, w))
           chol_arrow2_rl<T, DIM>(H, g, dir);
@@ -4807,10 +4777,10 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
           chol_sparse_border<DIM>(M, w, H, g, dir);
       }
       PMARK(PH_NCHOL);
-    } else if (dense_mfma_chol<T, DIM>() && nv > 80 && !(M.dbg_flags & 3)) {  // hstride() pads these
+    } else if (dense_mfma_chol<T, DIM>() && nv > 80 && !(FM_XF(M) & 2)) {  // hstride() pads these; FM_CHOL_LDS=2: the sparse LDS factor
       if constexpr (dense_mfma_chol<T, DIM>()) chol_dense_mfma<DIM>(M, w, H, nv, g, dir);
       PMARK(PH_NCHOL);
-    } else if (!(M.dbg_flags & 1) && chol_sparse_lds(M, w, H, g, dir)) {
+    } else if (chol_sparse_lds(M, w, H, g, dir)) {
       PMARK(PH_NCHOL);
     } else {
       // dense Cholesky (right-looking over the column-major lower-triangle table)
@@ -4991,9 +4961,9 @@ __device__ __forceinline__ void newton(const Model<T>& M, const Ws<T, DIM>& w, i
   // final constraint forces at a
   contact_f3(w, ncon);
   SYNC();
-  if (scatter && !(M.dbg_flags & 4096))
+  if constexpr (scatter)
     gather_JtF_sc(M, w, ncon, nrow, w.fc(), tmp);
-  else if ((pc_scene<T, DIM>() || scatter) && !(M.dbg_flags & 64))
+  else if constexpr (pc_scene<T, DIM>())
     gather_JtF_pc(M, w, ncon, nrow, w.fc(), tmp);
   else
     gather_JtF(M, w, ncon, nrow, w.fc(), false);
@@ -5862,17 +5832,18 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
   for (int t = t0;; t++) {
     stage(M, w, arena, ctr);
     if constexpr (can_abandon) {
-      // uniform (LDS scalar); experiment switch 512 (FM_FORCE_RERUN=1): every env-step goes to the wide kernel
-      // switch 16384 (FM_RERUN_AT_50=1): every env-step abandoned at substep 50 (the resume path's parity test)
-      if (S.rerun && (w.misc()[MISC_OVF] > 0 || (M.dbg_flags & 512) || ((M.dbg_flags & 16384) && t == 50))) {
+      // uniform (LDS scalar); the experiment build's test hooks: FM_FORCE_RERUN=1 (512), every env-step goes to the
+      // wide kernel; FM_RERUN_AT_50=1 (16384), every env-step abandoned at substep 50 (the resume path's parity test)
+      if (S.rerun && (w.misc()[MISC_OVF] > 0 || (FM_XF(M) & 512) || ((FM_XF(M) & 16384) && t == 50))) {
         if (!reset_pass) {
           double* const rs = S.resume;
           if (rs) {
             // the substep state for the wide kernel to resume from (substeps 0 .. t-1 done; stage t is redone there)
             double* r = rs + (size_t)ARENA_ * resume_stride(dm.nq, dm.nv, nu);
             if (LANE == 0) {
+              // the contact demand of the stages before t: stage t is redone (and counted) by the wide kernel
               r[0] = (double)t;
-              r[1] = (double)w.misc()[MISC_CSUM];
+              r[1] = (double)(w.misc()[MISC_CSUM] - w.misc()[MISC_NSTAGE]);
               r[2] = (double)w.misc()[MISC_CMAX];
             }
             r += 3;
@@ -5889,13 +5860,10 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
             }
           }
           if (LANE == 0) {
-            // publish: the slot's store releases the resume record and the backup at device scope (the wide kernel
-            // may be running on another stream, on another XCD, and takes the slot as soon as it is nonzero)
+            // the wide kernel reads the list after this launch has ended (kernel boundary: no fence needed)
             int32_t* const rr = S.rerun;
             const int slot = atomicAdd(rr, 1);
-            __hip_atomic_store(rr + 1 + slot, arena + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            // ... and is ordered before this workgroup's (relaxed) count of finished workgroups
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            rr[1 + slot] = arena + 1;
           }
           return;
         }
@@ -6053,43 +6021,13 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
   (void)params;
   if constexpr (DIM::rerun) {
     // the wide-capacity rerun: the arenas the 64-contact launch abandoned, S.rerun[1 + i] - 1 for i < S.rerun[0],
-    // over the launch's workgroups (a small grid: the list is short, usually empty)
-    int32_t* const rr = kparams<StepParams<T>>().S.rerun;
-    int32_t* const done = kparams<StepParams<T>>().S.rdone;
-    if (!done) {  // serial: the 64-contact launch has ended
-      const int n = rr[0];
-      for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
-        step_arena<T, DIM, IK>(smem, rr[1 + i] - 1);
-        FULL_SYNC();
-      }
-    } else {
-      // concurrent: slot i is taken as soon as it is published; the wave ends when the 64-contact launch has ended
-      // and published no slot i (and, as a guard that every wave reaches, after 20 s of waiting)
-      const int nwg = kparams<StepParams<T>>().S.rdone_of;
-      const unsigned long long t_start = wall_clock64();
-      // The polls are relaxed device-scope loads (coherent reads, no cache maintenance); the acquire fence -- an
-      // invalidation of this XCD's L2, which the 64-contact waves sharing it depend on -- runs once per arena taken
-      // and once at the end, not per poll (polling with acquire loads cost the launch 11 %, profiles/r05m_*)
-      for (int i = (int)blockIdx.x; i < nwg; i += (int)gridDim.x) {  // at most one slot per 64-contact workgroup
-        int a = 0;
-        for (;;) {
-          a = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rr + 1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          if (a) break;
-          const int nd = __builtin_amdgcn_readfirstlane(__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          if (nd >= nwg) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            const int n = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (n <= i) break;
-            continue;  // published before the launch ended: its slot store is visible now
-          }
-          if (wall_clock64() - t_start > 2000000000ull) break;  // 20 s at 100 MHz
-          __builtin_amdgcn_s_sleep(127);
-        }
-        if (!a) break;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the resume record / backup the slot store released
-        step_arena<T, DIM, IK>(smem, a - 1);
-        FULL_SYNC();
-      }
+    // over the launch's workgroups (a small grid: the list is short, usually empty; it runs after the 64-contact launch
+    // on the same stream)
+    const int32_t* const rr = kparams<StepParams<T>>().S.rerun;
+    const int n = rr[0];
+    for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
+      step_arena<T, DIM, IK>(smem, rr[1 + i] - 1);
+      FULL_SYNC();
     }
   } else {
     // longest-processing-time-first dispatch: the host orders the arenas by their last env-step's duration, so the
@@ -6097,11 +6035,6 @@ __global__ void __launch_bounds__(64) FM_STEP_ATTR step_kernel(StepParams<T> par
     // on which workgroup steps an arena)
     const int32_t* const order_ = kparams<StepParams<T>>().S.order;
     step_arena<T, DIM, IK>(smem, order_ ? order_[blockIdx.x] : (int)blockIdx.x);
-    int32_t* const done = kparams<StepParams<T>>().S.rdone;
-    if (done) {  // concurrent rerun: relaxed (a release here would write back this XCD's L2 per workgroup); the
-                 // publishing workgroups fenced their slot store above
-      if (LANE == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 

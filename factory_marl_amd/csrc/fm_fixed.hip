@@ -1,7 +1,8 @@
 // fm_fixed.hip -- one compile-time scene (FM_A arms, FM_K objects): instantiates the env-step kernel
 // with FixedDims<FM_A, FM_K> (constexpr dims and LDS layout) for one precision (FM_PREC 32 or 64).  Built
 // once per scene and precision by the Makefile (fm_fixed_<A>_<K>_f<P>.o) so they compile in parallel.
-// FM_WIDE=1: the same scene's wide-capacity rerun kernel instead (fm_rerun_f<P>.o, the benchmark scene).
+// FM_WIDE=1: the same scene's wide-capacity rerun kernel instead (fm_rerun_f64.o, the benchmark scene; float64 for the
+// abandoned env-steps of both builds).
 #include "fm_device.hpp"
 
 #ifndef FM_WIDE
@@ -63,13 +64,10 @@ Lay rerun_layout() {
   return FixedDims<A, K, true>::template layout<sizeof(T)>();
 }
 
-// concurrent (alongside the 64-contact launch, State::rdone): 4 workgroups wait for published arenas -- an env-step
-// above 64 contacts is rare (about one arena in 60,000) and each waiting workgroup holds a wide workspace of LDS
 template <typename T, int A, int K>
-void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik, bool concurrent) {
+void rerun_launch(const StepParams<T>& p, int num_arenas, hipStream_t stream, bool ik) {
   const int lds = FixedDims<A, K, true>::template layout<sizeof(T)>().total;
-  const int cap = concurrent ? 1 : 256;
-  const dim3 grid(num_arenas < cap ? num_arenas : cap);
+  const dim3 grid(num_arenas < 256 ? num_arenas : 256);
   if (ik)
     hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K, true>, true>), grid, dim3(WAVE), lds, stream, p);
   else
@@ -80,7 +78,7 @@ static_assert(FixedDims<FM_A, FM_K, true>::template layout<sizeof(FM_REAL)>().to
               "wide rerun workspace exceeds the CU's LDS");
 template hipError_t rerun_set_attr<FM_REAL, FM_A, FM_K>();
 template Lay rerun_layout<FM_REAL, FM_A, FM_K>();
-template void rerun_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, hipStream_t, bool, bool);
+template void rerun_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, hipStream_t, bool);
 #else
 template hipError_t fixed_set_attr<FM_REAL, FM_A, FM_K>(int);
 template void fixed_launch<FM_REAL, FM_A, FM_K>(const StepParams<FM_REAL>&, int, int, hipStream_t, bool);

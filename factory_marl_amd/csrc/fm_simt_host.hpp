@@ -67,6 +67,9 @@ struct Wave {
 Wave& wave();
 int64_t cross(int op, int64_t a0, int64_t a1, int ctrl, int line = 0);  // deposit, rendezvous, result
 void mfma_16x16x4(float a, float b, const float* c, float* d);
+// a grid of `grid` emulated workgroups (fm_cpu.cpp), each lane running body(kernarg): the launch entry of the
+// compile-time scene objects (fm_cpu_fixed.cpp)
+void launch_kernel(unsigned grid, size_t lds_bytes, const void* kernarg, void (*body)(const void*));
 
 inline int lane() { return wave().lane; }
 inline Dim3 thread_idx() { return Dim3{(unsigned)lane(), 0u, 0u}; }
@@ -191,16 +194,6 @@ FM_NO_TSAN inline X atomicOr(X* p, Y v) {
   *p = (X)(o | (X)v);
   return o;
 }
-
-// scoped atomics of the concurrent wide rerun (fixed-dims kernels only; the CPU backend runs the runtime-dims
-// kernel, which only reads State::rdone as null)
-#ifndef __HIP_MEMORY_SCOPE_AGENT
-#define __HIP_MEMORY_SCOPE_AGENT 3
-#endif
-#define __hip_atomic_load(p, order, scope) (*(p))
-#define __hip_atomic_store(p, v, order, scope) (void)(*(p) = (v))
-#define __hip_atomic_fetch_add(p, v, order, scope) atomicAdd((p), (v))
-#define __builtin_amdgcn_s_sleep(n) ((void)0)
 
 // the MFMA builtin: v_mfma_f32_16x16x4_f32 over the wave (A: lane l gives A[l % 16][l / 16]; B: B[l / 16][l % 16];
 // C / D: lane l holds rows 4 (l / 16) .. + 3 of column l % 16)

@@ -38,13 +38,12 @@ ENV_CLASSES = {
 TOGGLE_CLASSES = envs.TOGGLE_CLASSES
 
 # env attributes with a value on the GPU path (base_env.py:133-147, environments.py:276-282):
-# the kernel's experiment switches (fm_api.hip read_experiment_flags): (environment variable, value) -> flag bit
-EXPERIMENT_FLAGS = {("FM_CHOL_LDS", "1"): 1, ("FM_CHOL_LDS", "2"): 2, ("FM_SERIAL_BOXBOX", "1"): 4,
-                    ("FM_NO_MIDCACHE", "1"): 8, ("FM_NO_ARROW", "1"): 16, ("FM_NO_ARROW", "2"): 32,
-                    ("FM_NO_SCATTER", "1"): 64, ("FM_SERIAL_FK", "1"): 128, ("FM_TWO_PASS_SETUP", "1"): 256,
-                    ("FM_FORCE_RERUN", "1"): 512, ("FM_NO_RERUN", "1"): 1024, ("FM_NO_TREEBLK", "1"): 2048,
-                    ("FM_PC_SCATTER", "1"): 4096, ("FM_TB_LDSBC", "1"): 8192, ("FM_RERUN_AT_50", "1"): 16384,
-                    ("FM_CONCURRENT_RERUN", "1"): 32768}
+# the experiment build's switches (libfactorysim_exp.so, fm_api.hip read_experiment_flags; the product library has
+# none): (environment variable, value) -> flag bit.  The reference forms of the kernel's exact reformulations (the
+# equivalence tests) and the rerun path's test hooks
+EXPERIMENT_FLAGS = {("FM_CHOL_LDS", "2"): 2, ("FM_SERIAL_BOXBOX", "1"): 4, ("FM_NO_MIDCACHE", "1"): 8,
+                    ("FM_NO_ARROW", "1"): 16, ("FM_FORCE_RERUN", "1"): 512, ("FM_NO_RERUN", "1"): 1024,
+                    ("FM_NO_TREEBLK", "1"): 2048, ("FM_RERUN_AT_50", "1"): 16384}
 
 # global scalars of the handle (fm_set_param), per-arena values of the state record, fixed at creation
 RUNTIME_PARAMS = ("pt_time", "initial_conveyor_speed", "conveyor_acceleration", "force_contact_threshold",
@@ -100,7 +99,7 @@ def _specs_from_env_fns(env_fns):
 class FactoryVecEnv:
     def __init__(self, num_envs, env_class="AllFullRLProgressRewardEnv", env_kwargs=None, device=0,
                  precision="fp32", seeds=None, return_numpy=True, max_contacts=0, solver_tolerance=0.0,
-                 solver_iterations=0, obs_dtype=None):
+                 solver_iterations=0, obs_dtype=None, experimental=False):
         import torch
 
         self.torch = torch
@@ -116,7 +115,8 @@ class FactoryVecEnv:
             raise ValueError(f"env_class {env_class!r} not implemented on the GPU path; available: {sorted(ENV_CLASSES)}")
         self.env_class = env_class
         self.progress = env_class in envs.PROGRESS_CLASSES
-        L = _lib.load()
+        # experimental: the experiment build of the library (set_experiment's switches compiled in; tests / A/B only)
+        L = _lib.load(experimental)
         cfg = _lib.FmConfig()
         L.fm_config_default(C.byref(cfg))
         cfg.num_arenas = int(num_envs)
@@ -162,9 +162,10 @@ class FactoryVecEnv:
         self.cpu = self.device.type == "cpu"
         h = C.c_void_p()
         _lib.check(L.fm_create(C.byref(cfg), -1 if self.cpu else (self.device.index or 0),
-                               seeds.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(h)))
+                               seeds.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(h)), L)
         self._h = h
         self._L = L
+        self.experimental = bool(experimental)
         self.num_envs = int(num_envs)
         self.precision = precision
         self.obs_dim = L.fm_obs_dim(h)
@@ -203,13 +204,16 @@ class FactoryVecEnv:
         self._user_attrs = [dict() for _ in range(n)]
 
     # ------------------------------------------------------------------ core API
+    def _check(self, rc):
+        _lib.check(rc, self._L)
+
     def _bind_stream(self):
         """run on torch's current stream so action / observation tensors are ordered with torch work"""
         if self.cpu:
             return
         s = self.torch.cuda.current_stream(self.device)
         if self._stream_bound != s.cuda_stream:
-            _lib.check(self._L.fm_set_stream(self._h, C.c_void_p(s.cuda_stream) if s.cuda_stream else None))
+            self._check(self._L.fm_set_stream(self._h, C.c_void_p(s.cuda_stream) if s.cuda_stream else None))
             self._stream_bound = s.cuda_stream
 
     def reset(self, mask=None):
@@ -218,7 +222,7 @@ class FactoryVecEnv:
         if mask is not None:
             m = self.torch.as_tensor(mask, dtype=self.torch.uint8, device=self.device).contiguous()
             mptr = C.c_void_p(m.data_ptr())
-        _lib.check(self._L.fm_reset(self._h, mptr, C.c_void_p(self.obs.data_ptr())))
+        self._check(self._L.fm_reset(self._h, mptr, C.c_void_p(self.obs.data_ptr())))
         now = time.time()
         self._t0 = [now] * self.num_envs
         return self.obs.cpu().numpy() if self.return_numpy else self.obs
@@ -235,7 +239,7 @@ class FactoryVecEnv:
             a = self.torch.zeros(max(self.num_envs, 1), dtype=self.torch.float32, device=self.device)
         self._actions = a
         self._bind_stream()
-        _lib.check(self._L.fm_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(self.obs.data_ptr()),
+        self._check(self._L.fm_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(self.obs.data_ptr()),
                                    C.c_void_p(self.rewards.data_ptr()), C.c_void_p(self.terminated.data_ptr()),
                                    C.c_void_p(self.truncated.data_ptr()), C.byref(self._info)))
         return self.obs, self.rewards, self.terminated, self.truncated
@@ -295,17 +299,20 @@ class FactoryVecEnv:
         return [int(i) for i in indices]
 
     def set_experiment(self, setting=""):
-        """the kernel's experiment switches on this live handle (A/B probes and equivalence tests only):
-        "FM_NO_ARROW=1 FM_NO_SCATTER=1" (EXPERIMENT_FLAGS) for the launches queued after the call; "" clears all"""
+        """the kernel's experiment switches on this live handle (A/B probes and equivalence tests only; a handle of the
+        experiment build, FactoryVecEnv(..., experimental=True)): "FM_NO_ARROW=1 FM_NO_MIDCACHE=1" (EXPERIMENT_FLAGS)
+        for the launches queued after the call; "" clears all"""
+        if not self.experimental and setting:
+            raise ValueError("experiment switches need the experiment build: FactoryVecEnv(..., experimental=True)")
         flags = 0
         for kv in (setting or "").split():
             k, v = kv.split("=")
             flags |= EXPERIMENT_FLAGS[(k, v)]
-        _lib.check(self._L.fm_set_param(self._h, b"experiment_flags", float(flags)))
+        self._check(self._L.fm_set_param(self._h, b"experiment_flags", float(flags)))
 
     def get_param(self, name):
         v = C.c_double()
-        _lib.check(self._L.fm_get_param(self._h, name.encode(), C.byref(v)))
+        self._check(self._L.fm_get_param(self._h, name.encode(), C.byref(v)))
         return float(v.value)
 
     def _arena_field(self, name):
@@ -358,7 +365,7 @@ class FactoryVecEnv:
             # init_spawn_freq is held per arm (v / A) and read back as (v / A) * A: compare to rounding
             if len(set(idx)) != self.num_envs and not math.isclose(v, self.get_param(name), rel_tol=1e-12, abs_tol=0.0):
                 raise ValueError(f"{name} is one value for all {self.num_envs} arenas of the batch: set it on every env")
-            _lib.check(self._L.fm_set_param(self._h, name.encode(), v))
+            self._check(self._L.fm_set_param(self._h, name.encode(), v))
             return
         if name in ARENA_SCALARS:
             st, A, K = self._arena_field(name)
@@ -433,7 +440,7 @@ class FactoryVecEnv:
         if frames:
             fr = torch.empty(len(idx), self._L.fm_render_ngeom(self._h), 20, dtype=torch.float32, device=self.device)
         cam = None if camera is None else (C.c_float * 6)(*[float(x) for x in camera])
-        _lib.check(self._L.fm_render(self._h, idx.ctypes.data_as(C.POINTER(C.c_int32)), len(idx), int(width),
+        self._check(self._L.fm_render(self._h, idx.ctypes.data_as(C.POINTER(C.c_int32)), len(idx), int(width),
                                      int(height), cam, C.c_void_p(img.data_ptr()),
                                      C.c_void_p(fr.data_ptr()) if fr is not None else None))
         return (img, fr) if frames else img
@@ -470,7 +477,7 @@ class FactoryVecEnv:
         return list(self._seeds)
 
     def sync(self):
-        _lib.check(self._L.fm_sync(self._h))
+        self._check(self._L.fm_sync(self._h))
 
     # ------------------------------------------------------------------ state / diagnostics
     def state_size(self):
@@ -479,7 +486,7 @@ class FactoryVecEnv:
     def get_state(self):
         self._bind_stream()
         buf = np.zeros(self.num_envs * self.state_size(), np.uint8)
-        _lib.check(self._L.fm_get_state(self._h, buf.ctypes.data_as(C.c_void_p)))
+        self._check(self._L.fm_get_state(self._h, buf.ctypes.data_as(C.c_void_p)))
         return buf.reshape(self.num_envs, -1)
 
     def set_state(self, buf):
@@ -487,12 +494,12 @@ class FactoryVecEnv:
         if not self.cpu:
             self.torch.cuda.synchronize(self.device)
         buf = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
-        _lib.check(self._L.fm_set_state(self._h, buf.ctypes.data_as(C.c_void_p)))
+        self._check(self._L.fm_set_state(self._h, buf.ctypes.data_as(C.c_void_p)))
 
     def counters(self):
         self._bind_stream()
         out = np.zeros((self.num_envs, _lib.num_counters(self._L)), np.int64)
-        _lib.check(self._L.fm_get_counters(self._h, out.ctypes.data_as(C.c_void_p)))
+        self._check(self._L.fm_get_counters(self._h, out.ctypes.data_as(C.c_void_p)))
         return out
 
     def costs(self):
@@ -500,20 +507,20 @@ class FactoryVecEnv:
         dispatch order is sorted by these)"""
         self._bind_stream()
         out = np.zeros(self.num_envs, np.uint32)
-        _lib.check(self._L.fm_get_costs(self._h, out.ctypes.data_as(C.c_void_p)))
+        self._check(self._L.fm_get_costs(self._h, out.ctypes.data_as(C.c_void_p)))
         return out
 
     def kernel_timing(self, enable=True):
         """time each env-step kernel launch alone (fm_kernel_timing: a HIP event pair on the env's stream around the
         step kernel; the dispatch-order kernel and the wide rerun launch stay outside)"""
         self._bind_stream()
-        _lib.check(self._L.fm_kernel_timing(self._h, 1 if enable else 0))
+        self._check(self._L.fm_kernel_timing(self._h, 1 if enable else 0))
 
     def kernel_time(self):
         """(summed milliseconds, launches) of the step-kernel launches since the last call (fm_get_kernel_time)"""
         self._bind_stream()
         ms, n = C.c_double(0.0), C.c_int(0)
-        _lib.check(self._L.fm_get_kernel_time(self._h, C.byref(ms), C.byref(n)))
+        self._check(self._L.fm_get_kernel_time(self._h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
     PHASES = ["fk", "geoms_mass", "collision", "rows", "smooth_acc", "newton_setup", "newton_grad",
@@ -526,7 +533,7 @@ class FactoryVecEnv:
         ({phase: seconds summed over arenas}, ncon summed over stages)"""
         self._bind_stream()
         out = np.zeros(24, np.uint64)
-        _lib.check(self._L.fm_profile(self._h, int(mode), out.ctypes.data_as(C.c_void_p)))
+        self._check(self._L.fm_profile(self._h, int(mode), out.ctypes.data_as(C.c_void_p)))
         khz = float(out[15]) or 1.0
         return {p: float(out[i]) / (khz * 1e3) for i, p in enumerate(self.PHASES) if p}, int(out[14])
 
@@ -536,7 +543,7 @@ class FactoryVecEnv:
         buf = np.zeros(200000)
         n = self._L.fm_debug_dump(self._h, arena, int(actuated), buf.ctypes.data_as(C.c_void_p), len(buf))
         if n < 0:
-            _lib.check(n)
+            self._check(n)
         out = {}
         o = 0
 

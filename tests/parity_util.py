@@ -130,6 +130,8 @@ def compare(trajectory, precision, A, K, env_class="AllFullRLProgressRewardEnv",
     alt_outs = alt[2] if alt is not None else None
     n = len(recs)
     experiment = kw.pop("experiment", "")
+    if experiment:
+        kw["experimental"] = True  # the switches live in the experiment build of the library
     env = gpu_env(n, precision, A, K, env_class, **kw)
     if experiment:
         env.set_experiment(experiment)  # kernel experiment switches (FactoryVecEnv.set_experiment)

@@ -81,9 +81,12 @@ def test_vec_env_raises_without_library(monkeypatch, tmp_path):
     from factory_marl_amd import _lib
 
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
-    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setattr(_lib, "EXP_LIB_PATH", str(tmp_path / "missing_exp.so"))
+    monkeypatch.setattr(_lib, "_LIBS", {})
     with pytest.raises(_lib.FactorySimError):
         _lib.load()
+    with pytest.raises(_lib.FactorySimError):
+        _lib.load(experimental=True)
 
 
 def test_state_record_roundtrip():

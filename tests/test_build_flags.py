@@ -46,11 +46,11 @@ def test_sync_is_a_wave_barrier_with_fences():
     assert "__ATOMIC_RELEASE" in body and "__ATOMIC_ACQUIRE" in body and '"wavefront"' in body
 
 
-def _isa():
+def _isa(name="libfactorysim.so"):
     import importlib.util
 
     root = pathlib.Path(__file__).resolve().parents[1]
-    so = root / "factory_marl_amd" / "libfactorysim.so"
+    so = root / "factory_marl_amd" / name
     if not so.exists() or not pathlib.Path("/opt/rocm/lib/llvm/bin/llvm-objdump").exists():
         import pytest
 
@@ -102,3 +102,49 @@ def test_benchmark_kernel_does_not_spill():
     v = k[0][2]
     assert v["vgpr_spill_count"] == 0 and v["private_segment_fixed_size"] == 0, v
     assert v["vgpr_count"] + v.get("agpr_count", 0) <= 256, v
+
+
+def test_product_kernels_carry_no_experiment_switches():
+    """the A/B and test switches live in the experiment build only (libfactorysim_exp.so, -DFM_EXPERIMENTS=1): in the
+    kernel sources every switch is read through FM_XF(M), the constant 0 in the product build, and Model has no
+    dbg_flags field there -- so the product's step kernels take a smaller parameter block than the experiment build's
+    (the switch word is absent from their kernarg)"""
+    src = DEVICE.read_text()
+    assert "dbg_flags" not in src and "FM_XF(M)" in src
+    dev = (DEVICE.parent / "fm_dev.hpp").read_text()
+    m = re.search(r"#if FM_EXPERIMENTS\n\s*int dbg_flags;.*?\n#endif", dev)
+    assert m, "Model::dbg_flags must be compiled only into the experiment build"
+    assert re.search(r"#else\n#define FM_XF\(M\) 0\n", dev)
+    _, meta = _scan()
+    _, meta_x = _isa("libfactorysim_exp.so")
+    name = "void fm::step_kernel<float, fm::FixedDims<2, 4, false>, false>"
+    k = [v for (co, n), v in meta.items() if n.startswith(name)]
+    kx = [v for (co, n), v in meta_x.items() if n.startswith(name)]
+    assert len(k) == 1 and len(kx) == 1
+    assert k[0]["kernarg_segment_size"] < kx[0]["kernarg_segment_size"], (k[0], kx[0])
+
+
+def test_product_library_rejects_experiment_switches():
+    """a handle of the product library refuses the switches (FM_EINVAL), on the CPU backend (device = -1)"""
+    import ctypes as C
+
+    from factory_marl_amd import _lib
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    if not (root / "factory_marl_amd" / "libfactorysim.so").exists():
+        import pytest
+
+        pytest.skip("libfactorysim.so not built")
+    L = _lib.load()
+    cfg = _lib.FmConfig()
+    L.fm_config_default(C.byref(cfg))
+    cfg.num_arms, cfg.max_num_objects = 2, 4
+    h = C.c_void_p()
+    seeds = (C.c_uint64 * 1)(42)
+    _lib.check(L.fm_create(C.byref(cfg), -1, seeds, C.byref(h)), L)
+    try:
+        assert L.fm_set_param(h, b"experiment_flags", 512.0) != 0
+        assert b"compiled out" in L.fm_last_error()
+        assert L.fm_set_param(h, b"experiment_flags", 0.0) == 0
+    finally:
+        L.fm_destroy(h)

@@ -1,5 +1,6 @@
-"""The kernel's exact reformulations against their straightforward forms, on the GPU (experiment switches set on the
-live handle, FactoryVecEnv.set_experiment):
+"""The kernel's exact reformulations against their straightforward forms, on the GPU (experiment switches set on a
+live handle of the experiment build, FactoryVecEnv(..., experimental=True).set_experiment; the product library is
+compiled without them, and test_product_equals_experiment_build holds the two builds to the same bits):
 
 * the cached midphase (a body-pair list of an inflated test reused across substeps) against a rebuild at every
   substep (FM_NO_MIDCACHE=1): the contact set is the same by construction, so the trajectories are bit-identical;
@@ -31,7 +32,7 @@ def _run(A, K, n, steps, switch, precision="fp32", env_class="AllFullRLProgressR
 
     env = FactoryVecEnv(n, env_class=env_class, env_kwargs=run_kwargs(env_class, num_arms=A, max_num_objects=K,
                                                                       seed=42),
-                        precision=precision, seeds=42 + np.arange(n), return_numpy=False)
+                        precision=precision, seeds=42 + np.arange(n), return_numpy=False, experimental=True)
     env.reset()
     s0 = env.get_state()  # both runs start from this record (reset() continues the TaskManager RNG)
     g = torch.Generator(device=env.device)
@@ -89,7 +90,7 @@ def test_treeblock_solve_agrees_with_dense_and_sparse_4x16(other):
     A, K, n = 4, 16, 128
     env = FactoryVecEnv(n, env_class="PauseIKToggleEnv", env_kwargs=run_kwargs("PauseIKToggleEnv", num_arms=A,
                                                                                max_num_objects=K, seed=42),
-                        seeds=42 + np.arange(n), return_numpy=False)
+                        seeds=42 + np.arange(n), return_numpy=False, experimental=True)
     env.reset()
     g = torch.Generator(device=env.device)
     g.manual_seed(9)
@@ -128,7 +129,7 @@ def _one_step(A, K, n, pre, switch, value="1", precision="fp32", base=""):
     from factory_marl_amd.environments import run_kwargs
 
     env = FactoryVecEnv(n, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=A, max_num_objects=K, seed=42),
-                        precision=precision, seeds=42 + np.arange(n), return_numpy=False)
+                        precision=precision, seeds=42 + np.arange(n), return_numpy=False, experimental=True)
     env.reset()
     g = torch.Generator(device=env.device)
     g.manual_seed(11)
@@ -164,16 +165,6 @@ def test_two_pass_arrowhead_agrees_with_bordered_factor(A, K):
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-@pytest.mark.parametrize("precision", ["fp32", "fp64"])
-def test_one_pass_warmstart_products_are_exact(precision):
-    """(2,4): both warmstart candidates' row products in one pass (rows_eval2) against two separate passes
-    (FM_TWO_PASS_SETUP=1): the same products per row, so 40 env-steps of 256 arenas are bit-identical"""
-    a, b = _run(2, 4, 256, 40, "FM_TWO_PASS_SETUP", precision=precision)
-    assert np.array_equal(a, b)
-
-
-
-@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 @pytest.mark.parametrize("A,K", [(2, 8), (2, 10)])
 def test_treeblock_solve_agrees_with_dense_path(A, K):
     """fp32 (2,8) / (2,10): the tree-block Newton solve (the default) against the dense global-block Hessian with its
@@ -182,3 +173,30 @@ def test_treeblock_solve_agrees_with_dense_path(A, K):
     print(f"({A},{K}) tree-block vs dense path, one env-step from 256 states: median {np.median(errs):.2e}, "
           f"99th pct {np.quantile(errs, 0.99):.2e}, worst {errs.max():.2e}")
     assert np.median(errs) <= 1e-6 and np.mean(errs <= 1e-5) >= 0.99 and errs.max() <= 1e-4
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("precision,A,K", [("fp32", 2, 4), ("fp64", 2, 4), ("fp32", 2, 8)])
+def test_product_equals_experiment_build(precision, A, K):
+    """the product library (no switches: FM_EXPERIMENTS=0, every switch branch compiled out) and the experiment build
+    with every switch off step the same records to the same bits: the equivalence tests above, run on the experiment
+    build, speak for the product kernels"""
+    from factory_marl_amd import FactoryVecEnv
+    from factory_marl_amd.environments import run_kwargs
+
+    n, steps = 256, 30
+    out = []
+    for exp in (False, True):
+        env = FactoryVecEnv(n, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=A, max_num_objects=K,
+                                                     seed=42),
+                            precision=precision, seeds=42 + np.arange(n), return_numpy=False, experimental=exp)
+        env.reset()
+        g = torch.Generator(device=env.device)
+        g.manual_seed(3)
+        for _ in range(steps):
+            env.step_tensors(torch.rand(n, env.act_dim, device=env.device, generator=g) * 2 - 1)
+        env.sync()
+        out.append((env.get_state(), env.counters()))
+        env.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])

@@ -139,31 +139,6 @@ def test_fp32_against_mujoco_tolerance_oracle(oracle):
         assert frac >= 0.99 and e.max() <= 5e-4, (frac, e.max())
 
 
-def _float_floor_states(traj, steps):
-    """per record in `steps`: the relative state error of the float restatement (liboracle_f32: the oracle's sources
-    in single precision) stepped from the record rounded to float32, against the float64 oracle's result"""
-    import os
-    import sys
-
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
-    import fp32_floor
-    from oracle import pyoracle as po
-
-    from factory_marl_amd import state as st
-
-    recs, acts, outs = traj
-    f = po.Env(A, K, 42, reward="progress", weights=(0.2, 0.4, 0.1, 0.4), f32=True)
-    f.reset()
-    out = []
-    for k in steps:
-        d, i, rg = st.unpack(A, K, recs[k])
-        f.import_state(d.astype(np.float32), i, rg)
-        f.step(acts[k])
-        f2, _, _ = f.export_state()
-        out.append(fp32_floor.rel_err(A, K, f2.astype(np.float64), outs[k]["dbl"]))
-    return np.array(out)
-
-
 def _float_floor(A_, K_, T, seed):
     import os
     import sys
@@ -409,9 +384,10 @@ def test_ik_timing_follows_control_frequency_and_pt_time(oracle):
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
 def test_wide_rerun_kernel_matches_oracle(trajectory, precision):
-    """the (2,4) scene's wide-capacity rerun kernel (FixedDims<2, 4, true>) on every env-step of the 96-step
-    trajectory (FM_FORCE_RERUN=1: the 64-contact launch abandons each arena at its first stage): the same gates as
-    the 64-contact kernel -- fp64 within 1e-7, fp32 the SURVEY gate on >= 98.5 %, integer state exact"""
+    """the (2,4) scene's wide-capacity rerun kernel (FixedDims<2, 4, true>, float64 for both builds) on every env-step
+    of the 96-step trajectory (FM_FORCE_RERUN=1: the 64-contact launch abandons each arena at its first stage): the
+    same gates as the 64-contact kernel -- fp64 within 1e-7, the fp32 handle (its abandoned env-steps stepped in
+    float64 at MuJoCo's 1e-8 Newton tolerance) the SURVEY gate on >= 98.5 %, integer state exact"""
     r = pu.compare(trajectory, precision, A, K, experiment="FM_FORCE_RERUN=1")
     e = r["errs"]
     print(f"{precision} wide rerun: worst {e.max():.2e}, within 1e-4 {np.mean(e <= 1e-4):.1%}, reruns "
@@ -422,20 +398,6 @@ def test_wide_rerun_kernel_matches_oracle(trajectory, precision):
         assert e.max() <= 1e-7 and r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
     else:
         assert np.mean(e <= 1e-4) >= 0.985 and e.max() <= 5e-4
-
-
-@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
-@pytest.mark.parametrize("resume", [False, True])
-def test_concurrent_wide_rerun_matches_oracle(trajectory, resume):
-    """the experiment FM_CONCURRENT_RERUN=1 (the wide kernel on a side stream, taking each abandoned arena as the
-    64-contact launch publishes it): every env-step abandoned at its first stage, or at substep 50 and
-    resumed there -- the serial rerun's fp64 gates, every arena stepped once by the wide kernel"""
-    exp = ("FM_RERUN_AT_50=1" if resume else "FM_FORCE_RERUN=1") + " FM_CONCURRENT_RERUN=1"
-    r = pu.compare(trajectory, "fp64", A, K, experiment=exp)
-    e = r["errs"]
-    assert not r["flag_bad"] and not r["int_bad"], (r["flag_bad"], r["int_bad"])
-    assert int(r["counters"][:, 8].sum()) == len(trajectory[0])
-    assert e.max() <= 1e-7 and r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
 
 
 def _crowded_states(oracle, n_states, lo=66, hi=110, seed=0):
@@ -483,10 +445,19 @@ def test_wide_rerun_resumes_at_the_abandoned_substep(trajectory, precision):
     fp32 the SURVEY gate on >= 98.5 %, integer state and flags exact)"""
     r = pu.compare(trajectory, precision, A, K, experiment="FM_RERUN_AT_50=1")
     e = r["errs"]
+    # the episode-mix counters of the resumed env-steps: contacts summed over the stages (ctr[4]: stage 50 is counted
+    # once, by the wide kernel that redoes it) and the largest stage (ctr[5]), against the uninterrupted kernel
+    ref = pu.compare(trajectory, precision, A, K)
+    same4 = float(np.mean(r["counters"][:, 4] == ref["counters"][:, 4]))
     print(f"{precision} resumed at substep 50: worst {e.max():.2e}, within 1e-4 {np.mean(e <= 1e-4):.1%}, reruns "
-          f"{int(r['counters'][:, 8].sum())}")
+          f"{int(r['counters'][:, 8].sum())}, contact sums equal to the uninterrupted run's on {same4:.1%} of arenas")
     assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"], r["reset_bad"])
     assert int(r["counters"][:, 8].sum()) == len(trajectory[0])
+    if precision == "fp64":
+        assert np.array_equal(r["counters"][:, 4], ref["counters"][:, 4])
+        assert np.array_equal(r["counters"][:, 5], ref["counters"][:, 5])
+    else:  # the fp32 handle's stages 50-99 run in float64 here: a marginal contact may differ, not a whole stage's
+        assert same4 >= 0.9 and np.abs(r["counters"][:, 4] - ref["counters"][:, 4]).max() <= 8
     if precision == "fp64":
         assert e.max() <= 1e-7 and r["obs_err"].max() <= 1e-5 and r["rew_err"].max() <= 1e-6
     else:
@@ -590,11 +561,12 @@ def crowded(oracle):
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
 def test_contacts_above_64_are_not_dropped(crowded, precision):
     """(2,4) benchmark scene, env-steps whose stages hold more than 64 contacts (arms reaching into the table, the belt
-    and each other; the parked cubes' 16 floor contacts): the 64-contact launch abandons them and the wide kernel
-    steps them -- no contact is dropped, and from the same records the oracle (which keeps every contact,
+    and each other; the parked cubes' 16 floor contacts): the 64-contact launch abandons them and the (float64) wide
+    kernel steps them -- no contact is dropped, and from the same records the oracle (which keeps every contact,
     base_env.py:217-218 -> mj_step) gives the same result.  >= 8 of the records do not terminate, so they are
-    compared as states: fp64 within 1e-7; fp32 (the wide kernel of the benchmarked build) at the SURVEY gate against
-    the nearer of the 1e-12 / 1e-8 oracles; integer state / flags exact in both"""
+    compared as states: fp64 within 1e-7; the fp32 handle (the benchmarked build, whose abandoned env-steps run in
+    float64 at MuJoCo's 1e-8 Newton tolerance) at the SURVEY gate against the nearer of the 1e-12 / 1e-8 oracles on
+    >= 99 % of the states and within 1e-3 on every one; integer state / flags exact in both"""
     traj, tol8 = crowded
     recs = traj[0]
     r = pu.compare(traj, precision, A, K, alt=tol8 if precision == "fp32" else None, verbose_tol=1e-4)
@@ -610,19 +582,10 @@ def test_contacts_above_64_are_not_dropped(crowded, precision):
         assert e.max() <= 1e-7
         assert r["obs_err"].max() <= 1e-5
     else:
-        # arms pressed into / resting on the table and belt in 60-100 stiff contacts, the gripper plates' small masses
-        # among them: an fp32 rounding of the contact data moves these solves far more than a free-running env-step
-        # (round 5: the fp32 wide kernel holds the SURVEY gate on half of these states, worst 2.7e-3 .. 2.7e-2 across
-        # builds, gpurun_out/r05a, r05d).  The same algorithm in plain single precision (liboracle_f32) is off by
-        # 1.2e-2 .. 45 relative on them: the kernel must beat it on every state, and stay within 5e-2
-        em = r["errs_min"]
-        within = float(np.mean(em <= 1e-4))
-        ff = _float_floor_states(traj, r["err_steps"])
-        print(f"  nearer of the two oracles: {within:.1%} within 1e-4, worst {em.max():.2e}; float restatement "
-              f"{np.mean(ff <= 1e-4):.1%} within, median {np.median(ff):.2e}, per state "
-              f"{[(int(k), float('%.2e' % a), float('%.2e' % b)) for k, a, b in zip(r['err_steps'], e, ff)]}")
-        assert within >= 0.4 and em.max() <= 5e-2, (within, em.max())
-        assert np.all(e <= np.maximum(ff, 1e-4)), [(int(s), float(a), float(b)) for s, a, b in zip(r["err_steps"], e, ff)]
+        # round 5 stepped these in float32 (a float32 Hessian of 60-100 stiff contacts with the gripper plates' small
+        # masses among them: 8 of 12 states within the gate, worst 2.7e-2); the abandoned env-steps now run in float64
+        within, worst, missing = pu.two_oracle_gate(r, frac=0.99, cap=1e-3)
+        print(f"  nearer of the two oracles: {within:.1%} within 1e-4, worst {worst:.2e}, missing {missing}")
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")

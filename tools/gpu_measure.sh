@@ -11,6 +11,7 @@
 #   tests       pytest -m gpu (verbose, prints kept)          sweep32 / sweep64   parity sweep fp32 / fp64
 #   bench       default bench line (with the CPU baseline)    quick               bench, 30 steps, no CPU leg
 #   c3 c4 c5    config 3 / 4 (one GPU) / 5 benches             ktrace              rocprofv3 kernel trace + stats
+#   ktrace3 pmc3 / ktrace5 pmc5   config 3 / 5 kernel stats (+ PMC passes)
 #   pmc         PMC passes (FETCH, WRITE, SQ, VALU) + summaries
 #   phase       phase profiles (2,4) fp32 / fp64, (2,8), (4,16)     phase24   (2,4) fp32 only
 #   pmcsq       the SQ counter pass alone (waits, LDS bank conflicts)      pmcic   instruction-cache counters
@@ -119,6 +120,35 @@ for l in open('$O/$step$S.jsonl'):
           --last 2 --out $O/pmc5_valu$S.json || fail valu5 $?
         python tools/pmc_sq.py $(find $O/pmc5_sq$S -name "*counter_collection.csv" | head -1) $O/pmc5_sq_summary$S.json \
           || fail sq5 $?
+      fi ;;
+    ktrace3|pmc3)
+      # config 3's kernel ((2,8) AllFullRL fp32, 16384 arenas on one GPU, PPO rollout): kernel stats, then the PMC passes
+      P3="--workload config3 --steps 3 --warmup 1 --preroll 50 --ppo-epochs 1 --no-cpu-baseline"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace3$S -- python3 bench.py \
+        --workload config3 --steps 8 --warmup 2 --no-cpu-baseline > $O/ktrace3$S.log 2>&1 || fail ktrace3 $? $O/ktrace3$S.log
+      find $O/ktrace3$S -name "*kernel_stats.csv" | head -1 | xargs -r head -4
+      if [ $step = pmc3 ]; then
+        timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc3_fetch$S -- python3 bench.py $P3 \
+          > $O/pmc3_fetch$S.log 2>&1 || fail pmc3_fetch $? $O/pmc3_fetch$S.log
+        timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc3_write$S -- python3 bench.py $P3 \
+          > $O/pmc3_write$S.log 2>&1 || fail pmc3_write $? $O/pmc3_write$S.log
+        timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+          SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $O/pmc3_sq$S -- python3 bench.py $P3 \
+          > $O/pmc3_sq$S.log 2>&1 || fail pmc3_sq $? $O/pmc3_sq$S.log
+        timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 \
+          SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d $O/pmc3_valu$S -- python3 \
+          bench.py $P3 > $O/pmc3_valu$S.log 2>&1 || fail pmc3_valu $? $O/pmc3_valu$S.log
+        timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
+          SQ_INSTS_VALU_TRANS_F64 SQ_WAVES --output-format csv -d $O/pmc3_valu64$S -- python3 \
+          bench.py $P3 > $O/pmc3_valu64$S.log 2>&1 || fail pmc3_valu64 $? $O/pmc3_valu64$S.log
+        python tools/pmc_traffic.py $(find $O/pmc3_fetch$S -name "*counter_collection.csv" | head -1) \
+          $(find $O/pmc3_write$S -name "*counter_collection.csv" | head -1) --arenas 16384 --arms 2 --objects 8 \
+          --out $O/pmc3_traffic$S.json || fail traffic3 $?
+        python tools/pmc_valu.py $(find $O/pmc3_valu$S -name "*counter_collection.csv" | head -1) \
+          --f64 $(find $O/pmc3_valu64$S -name "*counter_collection.csv" | head -1) --arenas 16384 --arms 2 --objects 8 \
+          --last 3 --out $O/pmc3_valu$S.json || fail valu3 $?
+        python tools/pmc_sq.py $(find $O/pmc3_sq$S -name "*counter_collection.csv" | head -1) $O/pmc3_sq_summary$S.json \
+          || fail sq3 $?
       fi ;;
     phase24)
       timeout -k 10 200 python tools/phase_profile.py --precision fp32 > $O/phase_fp32$S.json 2> $O/phase$S.err \

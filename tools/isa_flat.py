@@ -69,7 +69,7 @@ def kernel_meta(co_path):
             continue
         d = {}
         for k in ("vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
-                  "private_segment_fixed_size", "group_segment_fixed_size"):
+                  "private_segment_fixed_size", "group_segment_fixed_size", "kernarg_segment_size"):
             mm = re.search(r"\.%s:\s+(\d+)" % k, blk)
             if mm:
                 d[k] = int(mm.group(1))

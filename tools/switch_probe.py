@@ -39,7 +39,7 @@ def main():
     for prec in args.precisions.split(","):
         n = args.arenas
         env = FactoryVecEnv(n, env_kwargs=run_kwargs("AllFullRLProgressRewardEnv", num_arms=2, max_num_objects=4, seed=42),
-                            precision=prec, seeds=42 + np.arange(n), return_numpy=False)
+                            precision=prec, seeds=42 + np.arange(n), return_numpy=False, experimental=True)
         env.reset()
         g = torch.Generator(device=env.device)
         g.manual_seed(3)
