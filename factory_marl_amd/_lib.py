@@ -69,8 +69,9 @@ EXPORTED = [
     "fm_act_dim", "fm_num_arenas", "fm_nq", "fm_nv", "fm_nu", "fm_workspace_bytes", "fm_reset", "fm_step", "fm_state_size",
     "fm_get_state", "fm_set_state", "fm_get_counters", "fm_debug_dump", "fm_profile", "fm_scene_mjcf",
     "fm_render", "fm_render_ngeom", "fm_set_param", "fm_get_param", "fm_num_counters", "fm_get_costs",
-    "fm_kernel_timing", "fm_get_kernel_time",
+    "fm_kernel_timing", "fm_get_kernel_time", "fm_abi_version", "fm_config_size",
 ]
+ABI_VERSION = 2  # include/factorysim.h FM_ABI_VERSION
 
 _LIBS = {}
 
@@ -89,6 +90,14 @@ def load(experimental=False):
         raise FactorySimError(f"{path} not built: run `python __graft_entry__.py build` (hipcc, gfx950)")
     L = C.CDLL(path)
     P, I = C.c_void_p, C.c_int
+    # the header this binding mirrors (FM_ABI_VERSION, sizeof(fm_config)) must be the library's
+    L.fm_abi_version.argtypes = []
+    L.fm_abi_version.restype = I
+    L.fm_config_size.argtypes = []
+    L.fm_config_size.restype = I
+    if L.fm_abi_version() != ABI_VERSION or L.fm_config_size() != C.sizeof(FmConfig):
+        raise FactorySimError(f"{path}: ABI version {L.fm_abi_version()} / fm_config {L.fm_config_size()} B, this "
+                              f"binding expects {ABI_VERSION} / {C.sizeof(FmConfig)} B (rebuild the library)")
     L.fm_config_default.argtypes = [C.POINTER(FmConfig)]
     L.fm_config_default.restype = None
     L.fm_create.argtypes = [C.POINTER(FmConfig), I, C.POINTER(C.c_uint64), C.POINTER(P)]

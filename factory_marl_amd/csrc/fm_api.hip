@@ -874,6 +874,9 @@ static int render_typed(fm_handle* h, int count, int width, int height, const Re
 
 extern "C" {
 
+int fm_abi_version(void) { return FM_ABI_VERSION; }
+int fm_config_size(void) { return (int)sizeof(fm_config); }
+
 void fm_config_default(fm_config* c) {
   std::memset(c, 0, sizeof *c);
   c->num_arenas = 1;

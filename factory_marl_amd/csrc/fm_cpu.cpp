@@ -23,7 +23,9 @@
 #include "fm_device.hpp"
 
 // ---------------------------------------------------------------------------------------------------------------
-// fibers (x86-64 System V: rbx, rbp, r12-r15, rsp, mxcsr and the x87 control word are callee-saved)
+// fibers (x86-64 System V: rbx, rbp, r12-r15 and rsp are callee-saved; mxcsr and the x87 control word too, but every
+// lane runs the same kernel code under the launching thread's floating-point environment, which nothing changes --
+// so the switch leaves them alone (the serialising ldmxcsr / fldcw pair cost ~40 % of a switch))
 // ---------------------------------------------------------------------------------------------------------------
 extern "C" void fm_simt_switch(void** save_sp, void* load_sp);
 extern "C" void fm_simt_trampoline();
@@ -41,14 +43,8 @@ fm_simt_switch:
   pushq %r13
   pushq %r14
   pushq %r15
-  subq $8, %rsp
-  stmxcsr (%rsp)
-  fnstcw 4(%rsp)
   movq %rsp, (%rdi)
   movq %rsi, %rsp
-  ldmxcsr (%rsp)
-  fldcw 4(%rsp)
-  addq $8, %rsp
   popq %r15
   popq %r14
   popq %r13
@@ -82,11 +78,6 @@ static void* fiber_init(char* stack, size_t bytes) {
   *--p = 0;                              // alignment pad
   *--p = (uint64_t)&fm_simt_trampoline;  // return address of fm_simt_switch
   for (int i = 0; i < 6; i++) *--p = 0;  // rbp rbx r12 r13 r14 r15
-  uint32_t csr;
-  uint16_t cw;
-  asm volatile("stmxcsr %0" : "=m"(csr));
-  asm volatile("fnstcw %0" : "=m"(cw));
-  *--p = (uint64_t)csr | ((uint64_t)cw << 32);
   return (void*)p;
 }
 
@@ -169,7 +160,7 @@ static void resolve(Wave& w) {
       break;
     }
   const int op = w.op[first];
-  static const bool trace = std::getenv("FACTORYSIM_CPU_TRACE") != nullptr;
+  static const bool trace = std::getenv("FACTORYSIM_CPU_TRACE") && !std::strcmp(std::getenv("FACTORYSIM_CPU_TRACE"), "ops");
   if (trace)
     std::fprintf(stderr, "[simt] block %u: %s 0x%x line %d (first live lane %d)\n", w.block.x, op_name(op),
                  w.ctrl[first], w.line[first], first);
@@ -259,15 +250,23 @@ static void run_block(Wave& w, unsigned b, unsigned grid, void (*entry)(void*), 
   w.lane = -1;  // between blocks: no lane runs
 }
 
+// the race / bounds detector build keeps guard zones around the emulated LDS: an access there is an out-of-bounds
+// workspace access (fm_race::access reports it; on the GPU it would read 0 or be dropped, silently)
+#ifdef FM_RACE_DETECT
+constexpr size_t LDS_GUARD = 64 * 1024;
+#else
+constexpr size_t LDS_GUARD = 0;
+#endif
 struct WaveBox {
   Wave w;
   std::unique_ptr<char[]> stacks;
   std::vector<char> lds;
-  WaveBox(size_t stack_bytes, size_t lds_bytes) : stacks(new char[stack_bytes * W]), lds(lds_bytes + 64) {
+  WaveBox(size_t stack_bytes, size_t lds_bytes)
+      : stacks(new char[stack_bytes * W]), lds(lds_bytes + 64 + 2 * LDS_GUARD) {
     std::memset(&w, 0, sizeof w);
     w.stacks = stacks.get();
     w.stack_bytes = stack_bytes;
-    w.lds = (char*)(((uintptr_t)lds.data() + 63) & ~(uintptr_t)63);
+    w.lds = (char*)(((uintptr_t)lds.data() + LDS_GUARD + 63) & ~(uintptr_t)63);
     w.lds_bytes = lds_bytes;
   }
 };
@@ -294,12 +293,17 @@ static void install_trace() {
   sa.sa_sigaction = segv_report;
   sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
   sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGILL, &sa, nullptr);  // -fsanitize-trap=bounds (the race / bounds detector build): an array index check
   static char altstack[1 << 16];
   stack_t ss{};
   ss.ss_sp = altstack;
   ss.ss_size = sizeof altstack;
   sigaltstack(&ss, nullptr);
 }
+
+// the rendezvous count of this host thread, carried over its launches of every kernel (the race detector's shadow
+// outlives a launch: an epoch must never repeat on a thread)
+static thread_local unsigned t_epoch = 0;
 
 // a grid of `grid` workgroups, spread over host threads; `entry(arg)` is the kernel body of one lane
 template <typename F>
@@ -314,9 +318,7 @@ static void launch(unsigned grid, size_t lds_bytes, const void* kernarg, F&& bod
     static const size_t stack_mb = std::getenv("FACTORYSIM_CPU_STACK_MB") ? std::atoi(std::getenv("FACTORYSIM_CPU_STACK_MB")) : 1;
     WaveBox box(stack_mb << 20, lds_bytes);
     box.w.lane = -1;
-    // the rendezvous count runs on over this thread's launches (the race detector's shadow outlives a launch)
-    static thread_local unsigned epoch = 0;
-    box.w.epoch = epoch;
+    box.w.epoch = t_epoch;
     t_wave = &box.w;
     box.w.kernarg = kernarg;
     struct Ctx {
@@ -329,7 +331,7 @@ static void launch(unsigned grid, size_t lds_bytes, const void* kernarg, F&& bod
       std::memset(box.w.lds, 0, lds_bytes);
       run_block(box.w, b, grid, entry, &ctx);
     }
-    epoch = box.w.epoch + 1;
+    t_epoch = box.w.epoch + 1;
     t_wave = nullptr;
   };
   if (nt <= 1) {
@@ -377,10 +379,18 @@ static thread_local std::unordered_map<uintptr_t, Shadow>* t_gshadow = nullptr;
 static thread_local unsigned t_gblock = ~0u;
 static thread_local const void* t_gwave = nullptr;
 static std::mutex g_mu;
-// (pc, other pc, kind 0 RAW 1 WAR 2 WAW) -> the first byte offset into LDS it was seen at (-1: global memory)
+// (pc, other pc, kind 0 RAW 1 WAR 2 WAW 3 LDS out of bounds 4 global scratch out of the arena's block) -> the first byte
+// offset into LDS it was seen at (-1: global memory; kind 4: the offset into the scratch buffer)
 static std::map<std::tuple<const void*, const void*, int>, long> g_races;
 static thread_local long t_off = -1;
 static int g_lay[sizeof(fm::Lay) / sizeof(int)];  // the LDS layout of the last step launch
+// the launch's per-arena global scratch blocks ([n][stride] bytes at base; fm_cpu_note_launch): every access there must
+// stay in the one block its workgroup's arena owns -- the first block a workgroup touches is its own
+static const char* g_spill = nullptr;
+static long long g_spill_stride = 0, g_spill_n = 0;
+static thread_local long long t_slot = -1;
+static thread_local unsigned t_slot_block = ~0u;
+static thread_local const void* t_slot_wave = nullptr;
 
 FM_NO_INSTR static void note(const void* pc, const void* other, int kind) {
   const bool was = t_in_hook;
@@ -395,6 +405,27 @@ FM_NO_INSTR static void access(const void* addr, size_t n, bool write, const voi
   fm_simt::Wave* w = fm_simt::t_wave;
   if (!w || !w->lds || t_in_hook || w->lane < 0) return;
   const char* a = (const char*)addr;
+  // bounds: the LDS guard zones (fm_simt::LDS_GUARD) and the arena's scratch block
+  if ((a + n > w->lds + w->lds_bytes && a < w->lds + w->lds_bytes + fm_simt::LDS_GUARD) ||
+      (a < w->lds && a + fm_simt::LDS_GUARD >= w->lds)) {
+    t_off = (long)(a - w->lds);
+    note(pc, nullptr, 3);
+    return;
+  }
+  if (g_spill && g_spill_stride > 0 && a >= g_spill && a < g_spill + g_spill_n * g_spill_stride) {
+    if (t_slot_block != w->block.x || t_slot_wave != (const void*)w) {
+      t_slot = -1;
+      t_slot_block = w->block.x;
+      t_slot_wave = w;
+    }
+    const long long off = (long long)(a - g_spill), slot = off / g_spill_stride;
+    const long long end_slot = (off + (long long)n - 1) / g_spill_stride;
+    if (t_slot < 0 && slot < g_spill_n) t_slot = slot;
+    if (slot != t_slot || end_slot != t_slot) {
+      t_off = (long)off;
+      note(pc, nullptr, 4);
+    }
+  }
   if (a < w->lds || a >= w->lds + w->lds_bytes) {
     // global memory: only addresses off this thread's stacks (the lanes' private variables live on the fibers)
     if (a >= w->stacks && a < w->stacks + (size_t)fm_simt::W * w->stack_bytes) return;
@@ -481,6 +512,17 @@ FM_RD(2)
 FM_RD(4)
 FM_RD(8)
 FM_RD(16)
+#define FM_URD(n)                                                                                             \
+  extern "C" FM_NO_INSTR void __tsan_unaligned_read##n(void* a) {                \
+    fm_race::access(a, n, false, __builtin_return_address(0));                                              \
+  }                                                                                                          \
+  extern "C" FM_NO_INSTR void __tsan_unaligned_write##n(void* a) {               \
+    fm_race::access(a, n, true, __builtin_return_address(0));                                               \
+  }
+FM_URD(2)
+FM_URD(4)
+FM_URD(8)
+FM_URD(16)
 extern "C" FM_NO_INSTR void __tsan_init() {}
 extern "C" FM_NO_INSTR void __tsan_func_entry(void*) {}
 extern "C" FM_NO_INSTR void __tsan_func_exit() {}
@@ -512,9 +554,10 @@ extern "C" FM_NO_INSTR int fm_race_report(char* out, int cap) {
   s += "\n";
   for (auto& r : fm_race::g_races) {
     char line[128];
+    const void* other = std::get<1>(r.first);  // null for the bounds kinds (3, 4): printed as 0
     std::snprintf(line, sizeof line, "%d 0x%lx 0x%lx %ld\n", std::get<2>(r.first),
                   (long)((const char*)std::get<0>(r.first) - (const char*)di.dli_fbase),
-                  (long)((const char*)std::get<1>(r.first) - (const char*)di.dli_fbase), r.second);
+                  other ? (long)((const char*)other - (const char*)di.dli_fbase) : 0L, r.second);
     s += line;
   }
   if (out && cap > 0) std::snprintf(out, (size_t)cap, "%s", s.c_str());
@@ -597,18 +640,32 @@ static void cpu_debug(const Model<T>& M, const State<T>& S, const Lay& L, int ar
 }  // namespace fm
 
 // entry points for fm_api.hip (the parameter blocks are the same structs, laid out from the same fm_dev.hpp)
-// the LDS layout of a step launch (tools/lds_race_check.py maps the racing offsets to its arrays; also called by the
-// compile-time scene objects, fm_cpu_fixed.cpp)
-extern "C" void fm_cpu_note_layout(const void* lay) {
+// the LDS layout and the scratch blocks of a step launch (tools/lds_race_check.py maps the racing offsets to the
+// layout's arrays; the bounds checks use both; also called by the compile-time scene objects, fm_cpu_fixed.cpp)
+extern "C" void fm_cpu_note_launch(const void* lay, const void* spill, long long stride, long long n) {
 #ifdef FM_RACE_DETECT
   std::memcpy(fm_race::g_lay, lay, sizeof(fm::Lay));
+  fm_race::g_spill = (const char*)spill;
+  fm_race::g_spill_stride = stride;
+  fm_race::g_spill_n = n;
 #else
   (void)lay;
+  (void)spill;
+  (void)stride;
+  (void)n;
 #endif
 }
+template <typename T>
+static void note_launch(const void* params, int num_arenas) {
+  const fm::StepParams<T>& p = *(const fm::StepParams<T>*)params;
+  fm_cpu_note_launch(&p.L, (const char*)p.S.spill, p.S.spill_stride, p.M.dm.N);
+  (void)num_arenas;
+}
 extern "C" void fm_cpu_step(int fp64, const void* params, int num_arenas, int lds_bytes, int ik) {
-  fm_cpu_note_layout(fp64 ? (const void*)&((const fm::StepParams<double>*)params)->L
-                          : (const void*)&((const fm::StepParams<float>*)params)->L);
+  if (fp64)
+    note_launch<double>(params, num_arenas);
+  else
+    note_launch<float>(params, num_arenas);
   if (fp64)
     fm::cpu_step<double>(*(const fm::StepParams<double>*)params, num_arenas, lds_bytes, ik != 0);
   else

@@ -15,7 +15,7 @@
 #define FM_CAT2(a, b, c) a##_##b##_##c
 #define FM_CAT(a, b, c) FM_CAT2(a, b, c)
 
-extern "C" void fm_cpu_note_layout(const void* lay);
+extern "C" void fm_cpu_note_launch(const void* lay, const void* spill, long long stride, long long n);
 
 namespace fm {
 
@@ -26,7 +26,9 @@ static void body(const void* p) {
 
 template <typename T, typename DIM>
 static void run(const void* params, int grid, int lds_bytes, bool ik) {
-  fm_cpu_note_layout(&((const StepParams<T>*)params)->L);
+  const StepParams<T>& p = *(const StepParams<T>*)params;
+  // the scratch blocks the kernel uses (none for the wide rerun kernel: its workspace is all LDS)
+  fm_cpu_note_launch(&p.L, DIM::spill ? (const char*)p.S.spill : nullptr, p.S.spill_stride, p.M.dm.N);
   ::fm_simt::launch_kernel((unsigned)grid, (size_t)lds_bytes, params, ik ? &body<T, DIM, true> : &body<T, DIM, false>);
 }
 

@@ -83,6 +83,14 @@ struct Dims {
   static constexpr bool rerun = false;      // see FixedDims<A, K, true>
   static constexpr bool f64arms = false;    // see FixedDims
   static constexpr bool gl_lists = false;   // see FixedDims
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_coll() {
+    return false;
+  }
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_sp() {
+    return false;
+  }
   static constexpr bool treeblk = false;    // see FixedDims
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
@@ -566,7 +574,8 @@ __host__ __device__ constexpr int tb_floats(int ntree) { return tb_sol(ntree) + 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
                                               bool midcache = false, bool nobc = false, bool f64arms = false,
-                                              bool gl_lists = false, bool treeblk = false, int tmask_words = 0) {
+                                              bool gl_lists = false, bool treeblk = false, int tmask_words = 0,
+                                              bool gl_stage = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -621,9 +630,11 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.cbw = take(tsize * 8 * ncb);
   if (!gl_lists) L.sp = take(4 * (ncb * (ncb - 1) / 2));  // every possible body pair can pass the midphase
   L.gsurv = take(4 * 4 * WAVE);
-  L.stage = take(tsize * 8 * maxcon);
-  L.skey = take(4 * maxcon);
-  L.spw = take(4 * maxcon);
+  if (!gl_stage) {
+    L.stage = take(tsize * 8 * maxcon);
+    L.skey = take(4 * maxcon);
+    L.spw = take(4 * maxcon);
+  }
   uend = off > uend ? off : uend;
   off = uend;
   L.c_i = take(4 * 4 * maxcon);
@@ -663,6 +674,14 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
         g += (8 * 90 * A + 255) & ~255;
       }
     }
+    if (gl_stage) {  // the staged contacts, their keys and pair words (the collision side of the phase-local union)
+      L.stage = g;
+      g += (tsize * 8 * maxcon + 255) & ~255;
+      L.skey = g;
+      g += (4 * maxcon + 255) & ~255;
+      L.spw = g;
+      g += (4 * maxcon + 255) & ~255;
+    }
     L.gtotal = g;
   }
   return L;
@@ -696,6 +715,9 @@ struct DimsSpill : Dims {
 #ifndef FM_TREEBLK
 #define FM_TREEBLK 1
 #endif
+#ifndef FM_GL_COLL
+#define FM_GL_COLL 0
+#endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
@@ -713,6 +735,16 @@ struct FixedDims {
   // the (4,16) scene also keeps its midphase hit list and float64 arm poses in the global block: 50.0 -> 37.9 KB of
   // LDS, four arenas per CU instead of three
   static constexpr bool gl_lists = spill && A_ == 4 && K_ == 16 && FM_GL_LISTS;
+  // the collision work lists -- staged contacts, keys, pair words and the midphase list -- in the global block too (the
+  // larger side of the phase-local union at (2,4) fp64, whose 29.9 KB of LDS hold 5 arenas per CU)
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_coll() {
+    return FM_GL_COLL && spill && A_ == 2 && K_ == 4 && !WIDE_ && TS == 8;
+  }
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_sp() {
+    return gl_lists || gl_coll<TS>();
+  }
   // the fp32 scenes with spilled records other than (2,4) solve the Newton system tree block by tree block
   // (newton_treeblk): their dense Hessian in the global block is only the fallback for more than TB_MAXR coupled
   // positions
@@ -731,7 +763,7 @@ struct FixedDims {
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
     return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms,
-                       gl_lists, treeblk);
+                       gl_sp<TS>(), treeblk, 0, gl_coll<TS>());
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -393,7 +393,7 @@ struct Ws {
   __device__ __forceinline__ uint32_t* sp() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (uint32_t*)((DIM::gl_lists ? gbase : base) + c.sp);
+      return (uint32_t*)((DIM::template gl_sp<sizeof(T)>() ? gbase : base) + c.sp);
     } else {
       return (uint32_t*)(base + L->sp);
     }
@@ -409,7 +409,7 @@ struct Ws {
   __device__ __forceinline__ T* stage() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.stage);
+      return (T*)((DIM::template gl_coll<sizeof(T)>() ? gbase : base) + c.stage);
     } else {
       return (T*)(base + L->stage);
     }
@@ -417,7 +417,7 @@ struct Ws {
   __device__ __forceinline__ int* skey() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (int*)(base + c.skey);
+      return (int*)((DIM::template gl_coll<sizeof(T)>() ? gbase : base) + c.skey);
     } else {
       return (int*)(base + L->skey);
     }
@@ -425,7 +425,7 @@ struct Ws {
   __device__ __forceinline__ uint32_t* spw() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (uint32_t*)(base + c.spw);
+      return (uint32_t*)((DIM::template gl_coll<sizeof(T)>() ? gbase : base) + c.spw);
     } else {
       return (uint32_t*)(base + L->spw);
     }
@@ -1543,7 +1543,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // when the cached list is reused, from w.mcache() (LDS): reads go through address-space-typed pointers chosen per
   // access, never through one pointer selected between the two (that would be generic: FLAT instructions)
   uint32_t* const sp = w.sp();
-  constexpr int SPAS = DIM::gl_lists ? AS_GLOBAL : AS_LDS;
+  constexpr int SPAS = DIM::template gl_sp<sizeof(T)>() ? AS_GLOBAL : AS_LDS;
   int nsp = 0, total = 0;
   bool reuse = false;
   T infl = T(0);

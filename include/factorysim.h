@@ -98,6 +98,14 @@ typedef struct fm_info {
 
 typedef struct fm_handle fm_handle;
 
+/* ABI version of this header and the size of the fm_config the library was built with: a binding built against a
+ * different header checks both before fm_create (version 2 appended fm_config.obs_float64; a caller passing the
+ * version-1 struct would leave it unset).  factory_marl_amd/_lib.py refuses a library whose version or fm_config size
+ * differs from its own. */
+#define FM_ABI_VERSION 2
+int fm_abi_version(void);
+int fm_config_size(void);
+
 void fm_config_default(fm_config* cfg);
 
 /* Create N arenas on `device`.  seeds: host array [N] -- per-arena seed used, as in the reference,

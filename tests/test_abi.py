@@ -44,6 +44,15 @@ def test_binding_registers_the_header_set():
     assert sorted(_lib.EXPORTED) == header_functions()
 
 
+def test_abi_version_and_config_size(lib):
+    """the library's ABI version and fm_config size are the header's (the binding checks both at load)"""
+    from factory_marl_amd import _lib
+
+    m = re.search(r"#define FM_ABI_VERSION (\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION == lib.fm_abi_version()
+    assert lib.fm_config_size() == C.sizeof(_lib.FmConfig)
+
+
 def test_config_defaults_match_the_reference(lib):
     from factory_marl_amd import _lib
 
