@@ -736,10 +736,11 @@ struct FixedDims {
   // LDS, four arenas per CU instead of three
   static constexpr bool gl_lists = spill && A_ == 4 && K_ == 16 && FM_GL_LISTS;
   // the collision work lists -- staged contacts, keys, pair words and the midphase list -- in the global block too (the
-  // larger side of the phase-local union at (2,4) fp64, whose 29.9 KB of LDS hold 5 arenas per CU)
+  // larger side of the phase-local union at (2,4)): FM_GL_COLL=1 the fp64 kernel (29.9 KB of LDS hold 5 arenas per CU),
+  // 2 both precisions
   template <int TS>
   __host__ __device__ static constexpr bool gl_coll() {
-    return FM_GL_COLL && spill && A_ == 2 && K_ == 4 && !WIDE_ && TS == 8;
+    return spill && A_ == 2 && K_ == 4 && !WIDE_ && (FM_GL_COLL == 2 || (FM_GL_COLL == 1 && TS == 8));
   }
   template <int TS>
   __host__ __device__ static constexpr bool gl_sp() {

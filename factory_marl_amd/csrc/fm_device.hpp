@@ -5662,12 +5662,17 @@ __global__ void __launch_bounds__(64) reset_kernel(Model<T> M, State<T> S, Lay L
 // IK: the env class may compose IK proposals (every class but AllFullRL); the AllFullRL instantiation carries
 // none of the IK code (and none of its register demand)
 #ifndef FM_WAVES_PER_EU
-#define FM_WAVES_PER_EU 0  // experiment builds: the minimum waves per SIMD the register allocation must allow
+#define FM_WAVES_PER_EU 0  // the minimum waves per SIMD the register allocation must allow (0: no constraint)
 #endif
-#if FM_WAVES_PER_EU > 0
-#define FM_STEP_ATTR __attribute__((amdgpu_waves_per_eu(FM_WAVES_PER_EU)))
-#else
+#ifndef FM_WAVES_PER_EU_IK
+#define FM_WAVES_PER_EU_IK FM_WAVES_PER_EU  // the same for the IK-class instantiation (step_kernel<T, DIM, true>)
+#endif
+#if defined(FM_HOST_SIMT) || (FM_WAVES_PER_EU == 0 && FM_WAVES_PER_EU_IK == 0)
 #define FM_STEP_ATTR
+#else
+#define FM_STEP_ATTR                                                                                    \
+  __attribute__((amdgpu_waves_per_eu(IK ? (FM_WAVES_PER_EU_IK > 0 ? FM_WAVES_PER_EU_IK : 1)           \
+                                        : (FM_WAVES_PER_EU > 0 ? FM_WAVES_PER_EU : 1))))
 #endif
 // one env-step of one arena on the calling wave (the body of step_kernel)
 template <typename T, typename DIM, bool IK>

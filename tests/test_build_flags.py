@@ -148,3 +148,41 @@ def test_product_library_rejects_experiment_switches():
         assert L.fm_set_param(h, b"experiment_flags", 0.0) == 0
     finally:
         L.fm_destroy(h)
+
+
+# VGPR spill ceilings of every step-kernel instantiation of the product library (code-object notes, round 6): the
+# benchmark kernel has none; the two-waves-per-SIMD kernels of (2,4) fp64 / IK classes and (2,8) / (2,10) AllFullRL
+# trade their spills for occupancy (measured: DESIGN.md §4 / §4c); the one-wave kernels keep only the few VGPRs the
+# non-inlined IK calls save.  A change that spills more than this is a regression to measure before it ships.
+SPILL_CEILING = {
+    "float, fm::FixedDims<2, 4, false>, false": 0,
+    "float, fm::FixedDims<2, 4, false>, true": 160,
+    "double, fm::FixedDims<2, 4, false>, false": 120,
+    "double, fm::FixedDims<2, 4, false>, true": 260,
+    "double, fm::FixedDims<2, 4, true>, false": 16,
+    "double, fm::FixedDims<2, 4, true>, true": 28,
+    "float, fm::FixedDims<2, 8, false>, false": 46,
+    "float, fm::FixedDims<2, 8, false>, true": 8,
+    "double, fm::FixedDims<2, 8, false>, false": 130,
+    "double, fm::FixedDims<2, 8, false>, true": 8,
+    "float, fm::FixedDims<2, 10, false>, false": 193,
+    "float, fm::FixedDims<2, 10, false>, true": 8,
+    "double, fm::FixedDims<2, 10, false>, false": 135,
+    "double, fm::FixedDims<2, 10, false>, true": 8,
+    "float, fm::FixedDims<4, 16, false>, false": 0,
+    "float, fm::FixedDims<4, 16, false>, true": 8,
+    "double, fm::FixedDims<4, 16, false>, false": 8,
+    "double, fm::FixedDims<4, 16, false>, true": 8,
+}
+
+
+def test_step_kernel_spills_within_their_ceilings():
+    _, meta = _scan()
+    seen = {}
+    for (co, n), v in meta.items():
+        m = re.match(r"void fm::step_kernel<(.*)>\(fm::StepParams", n)
+        if m and "FixedDims" in m.group(1):
+            seen[m.group(1)] = v["vgpr_spill_count"]
+    assert set(seen) == set(SPILL_CEILING), sorted(set(seen) ^ set(SPILL_CEILING))
+    over = {k: (v, SPILL_CEILING[k]) for k, v in seen.items() if v > SPILL_CEILING[k]}
+    assert not over, over
