@@ -559,6 +559,10 @@ static int create_typed(fm_handle* h) {
     h->spill_stride = h->lay_step.gtotal;
     HIPCHK(d_malloc(h, (void**)&h->spill_buf, (size_t)d.N * (size_t)h->lay_step.gtotal));
     h->allocs.push_back(h->spill_buf);
+    // the CPU backend's uninitialised-read probe (FACTORYSIM_CPU_POISON, fm_cpu.cpp): scratch blocks filled with the
+    // poison byte, as the GPU's hold whatever the allocation held
+    const char* pz = h->cpu ? getenv("FACTORYSIM_CPU_POISON") : nullptr;
+    if (pz) std::memset(h->spill_buf, atoi(pz), (size_t)d.N * (size_t)h->lay_step.gtotal);
   }
   // the benchmark scene at its 64-contact capacity: an env-step with a stage above it is rerun by the wide kernel
   // The wide kernel runs in float64 for both builds (an abandoned env-step is rare -- about one arena in 60,000 --

@@ -171,6 +171,22 @@ static void resolve(Wave& w) {
                    "lane %d: %s 0x%x at line %d)\n",
                    w.block.x, first, op_name(op), w.ctrl[first], w.line[first], l, op_name(w.op[l]), w.ctrl[l],
                    w.line[l]);
+      // the suspended lanes' call chains (frame pointers: an -O0 build), for llvm-symbolizer
+      for (int ln : {first, l}) {
+        const uint64_t* fr = (const uint64_t*)w.sp[ln];  // saved r15 r14 r13 r12 rbx rbp, return address
+        const uint64_t* bp = (const uint64_t*)fr[5];
+        Dl_info di{};
+        dladdr((const void*)fr[6], &di);
+        std::fprintf(stderr, "  lane %d: %s+0x%lx", ln, di.dli_fname ? di.dli_fname : "?",
+                     (long)((const char*)fr[6] - (const char*)di.dli_fbase));
+        for (int d = 0; d < 24 && bp; d++) {
+          const uint64_t ra = bp[1];
+          if (!ra) break;
+          std::fprintf(stderr, " 0x%lx", (long)((const char*)ra - (const char*)di.dli_fbase));
+          bp = (const uint64_t*)bp[0];
+        }
+        std::fprintf(stderr, "\n");
+      }
       std::abort();
     }
   switch (op) {
@@ -230,8 +246,15 @@ static void run_block(Wave& w, unsigned b, unsigned grid, void (*entry)(void*), 
   w.grid = Dim3{grid, 1u, 1u};
   w.entry = entry;
   w.entry_arg = arg;
+  // FACTORYSIM_CPU_POISON=<byte>: the top of every lane's stack (its locals at -O0) filled with that byte before the
+  // block runs -- the uninitialised-read probe (tools/poison_probe.py) compares the results of two poison values
+  static const int poison = std::getenv("FACTORYSIM_CPU_POISON") ? std::atoi(std::getenv("FACTORYSIM_CPU_POISON")) : -1;
   for (int l = 0; l < W; l++) {
     w.done[l] = false;
+    if (poison >= 0) {
+      const size_t top = std::min<size_t>(w.stack_bytes, 256 * 1024);
+      std::memset(w.stacks + (size_t)(l + 1) * w.stack_bytes - top, poison, top);
+    }
     w.sp[l] = fiber_init(w.stacks + (size_t)l * w.stack_bytes, w.stack_bytes);
   }
   static const bool reverse = std::getenv("FACTORYSIM_CPU_REVERSE") != nullptr;  // race probe: lanes in reverse order
@@ -328,7 +351,11 @@ static void launch(unsigned grid, size_t lds_bytes, const void* kernarg, F&& bod
     for (;;) {
       const unsigned b = next.fetch_add(1);
       if (b >= grid) break;
-      std::memset(box.w.lds, 0, lds_bytes);
+      // LDS starts zeroed (FACTORYSIM_CPU_POISON: filled with the poison byte -- the GPU's LDS holds whatever the
+      // previous workgroup left)
+      static const int lpoison =
+          std::getenv("FACTORYSIM_CPU_POISON") ? std::atoi(std::getenv("FACTORYSIM_CPU_POISON")) : 0;
+      std::memset(box.w.lds, lpoison, lds_bytes);
       run_block(box.w, b, grid, entry, &ctx);
     }
     t_epoch = box.w.epoch + 1;

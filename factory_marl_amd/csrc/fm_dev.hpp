@@ -91,6 +91,10 @@ struct Dims {
   __host__ __device__ static constexpr bool gl_sp() {
     return false;
   }
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_tbr() {
+    return false;
+  }
   static constexpr bool treeblk = false;    // see FixedDims
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
@@ -299,6 +303,7 @@ struct Lay {
   int mcache, mpos;  // cached midphase: uint32 [mc_cap(nv)] hit list, T [ncb][3] body positions at the build
   int bposd, bRd;    // fp32 scenes with DIM::f64arms: double [A][10][3], [A][10][9] arm body poses (narrowphase)
   int tblk;          // (2,8), (2,10), (4,16), (2,4) wide: the tree-block Newton solve's workspace (T, TB_*; Newton phase)
+  int tbr;           // with FixedDims::gl_tbr: its coupled system's matrix, a byte offset into the global block
   int total;
   // spill layouts (DimsSpill): H and c_r are byte offsets into the arena's global scratch block of gtotal bytes
   int spill, gtotal;
@@ -565,17 +570,22 @@ __host__ __device__ constexpr int hextra(int tsize, int nv) { return (tsize == 4
 // (TB_MAXR floats) -- their own slots: the solver's nv-double scratch w.tmp() is too small for them at (2,4)
 // (nv = 43 < 1.5 TB_MAXR)
 constexpr int TB_BLK = 54, TB_MAXR = 32;
+// (glr: the coupled system's matrix lives in the arena's global block instead, Lay::tbr)
 __host__ __device__ constexpr int tb_rest(int ntree) { return (TB_BLK * ntree + 3) & ~3; }
-__host__ __device__ constexpr int tb_map(int ntree) { return tb_rest(ntree) + TB_MAXR * TB_MAXR; }
-__host__ __device__ constexpr int tb_rhs(int ntree) { return (tb_map(ntree) + TB_MAXR + 3) & ~3; }  // 16-byte aligned
-__host__ __device__ constexpr int tb_sol(int ntree) { return tb_rhs(ntree) + 2 * TB_MAXR; }
-__host__ __device__ constexpr int tb_floats(int ntree) { return tb_sol(ntree) + TB_MAXR; }
+__host__ __device__ constexpr int tb_map(int ntree, bool glr = false) {
+  return tb_rest(ntree) + (glr ? 0 : TB_MAXR * TB_MAXR);
+}
+__host__ __device__ constexpr int tb_rhs(int ntree, bool glr = false) {  // 16-byte aligned
+  return (tb_map(ntree, glr) + TB_MAXR + 3) & ~3;
+}
+__host__ __device__ constexpr int tb_sol(int ntree, bool glr = false) { return tb_rhs(ntree, glr) + 2 * TB_MAXR; }
+__host__ __device__ constexpr int tb_floats(int ntree, bool glr = false) { return tb_sol(ntree, glr) + TB_MAXR; }
 
 __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int nu, int ngc, int ncb, int maxcon,
                                               int maxrow, int ntree, int tsize, bool spill = false,
                                               bool midcache = false, bool nobc = false, bool f64arms = false,
                                               bool gl_lists = false, bool treeblk = false, int tmask_words = 0,
-                                              bool gl_stage = false) {
+                                              bool gl_stage = false, bool gl_tbr = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -623,7 +633,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.g = take(8 * nv);
   L.Ma = take(8 * nv);
   L.tmp = take(8 * nv);
-  if (treeblk) L.tblk = take(tsize * tb_floats(ntree));
+  if (treeblk) L.tblk = take(tsize * tb_floats(ntree, gl_tbr));
   int uend = off;
   off = u0;
   L.gx = take(tsize * 4 * ngc);
@@ -674,6 +684,10 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
         g += (8 * 90 * A + 255) & ~255;
       }
     }
+    if (gl_tbr) {  // the tree-block solve's coupled system (assembled and factored only on coupled substeps)
+      L.tbr = g;
+      g += (tsize * TB_MAXR * TB_MAXR + 255) & ~255;
+    }
     if (gl_stage) {  // the staged contacts, their keys and pair words (the collision side of the phase-local union)
       L.stage = g;
       g += (tsize * 8 * maxcon + 255) & ~255;
@@ -716,7 +730,10 @@ struct DimsSpill : Dims {
 #define FM_TREEBLK 1
 #endif
 #ifndef FM_GL_COLL
-#define FM_GL_COLL 0
+#define FM_GL_COLL 1  // round 6: the (2,4) fp64 collision lists in the global block, 145.5k -> 164.3k env-steps/s fp64
+#endif
+#ifndef FM_GL28
+#define FM_GL28 0
 #endif
 template <int A_, int K_, bool WIDE_ = false>
 struct FixedDims {
@@ -740,7 +757,15 @@ struct FixedDims {
   // 2 both precisions
   template <int TS>
   __host__ __device__ static constexpr bool gl_coll() {
-    return spill && A_ == 2 && K_ == 4 && !WIDE_ && (FM_GL_COLL == 2 || (FM_GL_COLL == 1 && TS == 8));
+    return spill && !WIDE_ &&
+           ((A_ == 2 && K_ == 4 && (FM_GL_COLL == 2 || (FM_GL_COLL == 1 && TS == 8))) ||
+            (A_ == 2 && K_ == 8 && TS == 4 && FM_GL28));
+  }
+  // the tree-block solve's coupled system in the global block: with gl_coll, the fp32 (2,8) workspace drops from
+  // 26.7 to ~21 KB of LDS (7 arenas per CU instead of 6)
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_tbr() {
+    return spill && !WIDE_ && treeblk && A_ == 2 && K_ == 8 && TS == 4 && FM_GL28;
   }
   template <int TS>
   __host__ __device__ static constexpr bool gl_sp() {
@@ -764,7 +789,7 @@ struct FixedDims {
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
     return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms,
-                       gl_sp<TS>(), treeblk, 0, gl_coll<TS>());
+                       gl_sp<TS>(), treeblk, 0, gl_coll<TS>(), gl_tbr<TS>());
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

@@ -190,6 +190,18 @@ struct Ws {
       return (T*)(base + L->tblk);
     }
   }
+  // the tree-block solve's coupled system (LDS after the per-tree blocks, or the arena's global block: gl_tbr)
+  __device__ __forceinline__ T* tbr() const {
+    if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
+      constexpr Lay c = DIM::template layout<sizeof(T)>();
+      if constexpr (DIM::template gl_tbr<sizeof(T)>())
+        return (T*)(gbase + c.tbr);
+      else
+        return (T*)(base + c.tblk) + tb_rest(DIM::ntree);
+    } else {
+      return (T*)(base + L->tblk);  // runtime dims have no tree-block solve (never called)
+    }
+  }
   __device__ __forceinline__ T* fa() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
@@ -3005,18 +3017,19 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
     if (j == k) dinv = ri;
     if (j >= k) col[k] = lj;
     const unsigned ak = adj[tk];
-    if (j > k) {
-      static_for<0, NT>([&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        constexpr int ps = u == 0 ? NV - 1 : (u <= KK ? 6 * (u - 1) : A0 - 1 + 9 * (u - 1 - KK));
-        constexpr int pn = u == 0 ? 1 : (u <= KK ? 6 : 9);
-        if constexpr (ps + pn > k + 1) {                 // block not entirely at or above the pivot
-          if (u == tk || (ak & (1u << u))) {             // coupled to the pivot's tree
-            // the block's operands are broadcast first, then used: the v_readlane -> VALU hazard is paid once
-            // per block instead of once per entry
-            T lv[pn];
+    static_for<0, NT>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      constexpr int ps = u == 0 ? NV - 1 : (u <= KK ? 6 * (u - 1) : A0 - 1 + 9 * (u - 1 - KK));
+      constexpr int pn = u == 0 ? 1 : (u <= KK ? 6 : 9);
+      if constexpr (ps + pn > k + 1) {                 // block not entirely at or above the pivot
+        if (u == tk || (ak & (1u << u))) {             // coupled to the pivot's tree (uniform)
+          // the block's operands are broadcast first (uniform control flow: every cross-lane operation runs on the
+          // whole wave), then used by the lanes below the pivot: the v_readlane -> VALU hazard is paid once per
+          // block instead of once per entry
+          T lv[pn];
 #pragma unroll
-            for (int ii = 0; ii < pn; ii++) lv[ii] = ps + ii > k ? readlane(lj, ps + ii) : T(0);
+          for (int ii = 0; ii < pn; ii++) lv[ii] = ps + ii > k ? readlane(lj, ps + ii) : T(0);
+          if (j > k) {
 #pragma unroll
             for (int ii = 0; ii < pn; ii++) {
               const int i = ps + ii;
@@ -3024,8 +3037,8 @@ __device__ __forceinline__ void chol_sparse_rl(const Model<T>& M, const Ws<T, DI
             }
           }
         }
-      });
-    }
+      }
+    });
   });
   T acc = j < NV ? (T)-g[jo] : T(0);
   T y = T(0);
@@ -4377,8 +4390,9 @@ __device__ __forceinline__ bool newton_treeblk(const Model<T>& M, const Ws<T, DI
     return 6 * __popc(below & CUBES) + 9 * __popc(below & ~CUBES);
   };
   T* const tbw = w.tblk();
-  T* const R = tbw + tb_rest(NT);
-  int* const cmap = (int*)(tbw + tb_map(NT));
+  constexpr bool GR = DIM::template gl_tbr<sizeof(T)>();
+  T* const R = w.tbr();
+  int* const cmap = (int*)(tbw + tb_map(NT, GR));
   // ---- zero the blocks, belt rows and the coupled system; the coupled system's position map
   for (int e = LANE; e < TB_BLK * NT; e += WAVE) tbw[e] = 0.0f;
   for (int e = LANE; e < n * n; e += WAVE) R[e] = 0.0f;
@@ -4540,8 +4554,8 @@ __device__ __forceinline__ bool newton_treeblk(const Model<T>& M, const Ws<T, DI
   }
   const T S = wave_sum(s_t), LY = wave_sum(ly_t);
   // ---- the coupled system + belt (position m), in LDS with row stride n
-  double* const grest = (double*)(tbw + tb_rhs(NT));  // right-hand side (chol_solve_reg negates it)
-  T* const xr = tbw + tb_sol(NT);                  // its solution
+  double* const grest = (double*)(tbw + tb_rhs(NT, GR));  // right-hand side (chol_solve_reg negates it)
+  T* const xr = tbw + tb_sol(NT, GR);                  // its solution
   for (int e = LANE; e < n * n; e += WAVE) {
     const int i = e / n, j = e - n * (e / n);
     if (i < m && j < m) {

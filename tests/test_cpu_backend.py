@@ -133,3 +133,27 @@ np.save({repr(str(tmp_path / "out.npy"))}, env.get_state())
         assert np.array_equal(gi, ri) and np.array_equal(gr, rg), s
         qd, vd = pu.state_err(A, K, rd, gd)
         assert max(qd.max(), vd.max()) <= 1e-9, (s, qd.max(), vd.max())
+
+
+def test_crowded_states_through_the_wide_kernel_on_the_host(lib, oracle):
+    """(2,4) records whose first stage holds 66-110 contacts (arms pressed into the table, the belt and each other):
+    on the host, as on the GPU, the 64-contact kernel abandons them and the float64 wide kernel steps them
+    (fm_cpu_fixed.cpp); fp64 against the oracle within 1e-7, integer state / flags exact.  These env-steps also run
+    the general register factor (chol_sparse_rl: arms coupled to cubes), whose broadcasts round 6 moved out of a
+    lane-dependent branch -- the emulator stops on a cross-lane operation reached by part of the wave"""
+    import test_gpu_parity as tg
+
+    traj = tg._crowded_trajectory(oracle)
+    r = pu.compare(traj, "fp64", A, K, device="cpu")
+    assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"], r["reset_bad"])
+    assert int(r["counters"][:, 8].sum()) == len(traj[0]) and int(r["counters"][:, 0].sum()) == 0
+    assert r["errs"].max() <= 1e-7, r["errs"].max()
+
+
+def test_ik_grasps_on_the_host(lib, oracle):
+    """PauseIKToggleEnv over 96 env-steps (the IK base policy grasps cubes: arm-cube contacts couple two trees, the
+    non-arrowhead substeps) on the host against the oracle, fp64"""
+    tr = pu.rollout(oracle, A, K, 96, env_class="PauseIKToggleEnv", seed_actions=7)
+    r = pu.compare(tr, "fp64", A, K, env_class="PauseIKToggleEnv", device="cpu")
+    s = pu.summary(r)
+    assert s["int_bad"] == 0 and s["flag_bad"] == 0 and s["worst"] <= 1e-5, s
