@@ -24,12 +24,12 @@ static void body(const void* p) {
   step_kernel<T, DIM, IK>(*(const StepParams<T>*)p);
 }
 
-template <typename T, typename DIM>
+template <typename T, typename DIM, typename DIK = DIM>
 static void run(const void* params, int grid, int lds_bytes, bool ik) {
   const StepParams<T>& p = *(const StepParams<T>*)params;
   // the scratch blocks the kernel uses (none for the wide rerun kernel: its workspace is all LDS)
   fm_cpu_note_launch(&p.L, DIM::spill ? (const char*)p.S.spill : nullptr, p.S.spill_stride, p.M.dm.N);
-  ::fm_simt::launch_kernel((unsigned)grid, (size_t)lds_bytes, params, ik ? &body<T, DIM, true> : &body<T, DIM, false>);
+  ::fm_simt::launch_kernel((unsigned)grid, (size_t)lds_bytes, params, ik ? &body<T, DIK, true> : &body<T, DIM, false>);
 }
 
 }  // namespace fm
@@ -47,8 +47,8 @@ extern "C" int FM_CAT(fm_cpu_step_fixed, FM_A, FM_K)(int fp64, int wide, const v
 #endif
   }
   if (fp64)
-    fm::run<double, fm::FixedDims<FM_A, FM_K>>(params, grid, lds_bytes, ik != 0);
+    fm::run<double, fm::FixedDims<FM_A, FM_K>, fm::FixedDimsIK<double, FM_A, FM_K>>(params, grid, lds_bytes, ik != 0);
   else
-    fm::run<float, fm::FixedDims<FM_A, FM_K>>(params, grid, lds_bytes, ik != 0);
+    fm::run<float, fm::FixedDims<FM_A, FM_K>, fm::FixedDimsIK<float, FM_A, FM_K>>(params, grid, lds_bytes, ik != 0);
   return 0;
 }

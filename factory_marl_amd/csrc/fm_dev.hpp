@@ -82,6 +82,7 @@ struct Dims {
   static constexpr int MAXC = MAXCON_WIDE;  // upper bound of maxcon the code is built for
   static constexpr bool rerun = false;      // see FixedDims<A, K, true>
   static constexpr bool f64arms = false;    // see FixedDims
+  static constexpr bool f64gl = false;      // see FixedDims
   static constexpr bool gl_lists = false;   // see FixedDims
   template <int TS>
   __host__ __device__ static constexpr bool gl_coll() {
@@ -96,6 +97,10 @@ struct Dims {
     return false;
   }
   static constexpr bool treeblk = false;    // see FixedDims
+  template <int TS>
+  __host__ __device__ static constexpr bool treeblk_for() {
+    return false;
+  }
   int N, A, K, nq, nv, nu, ngc, nbox, npair, nparam, ntree, obs_dim, act_dim, frame_skip;
   int ncb, ncbp;  // collision bodies, allowed collision-body pairs
   int maxcon, maxrow;
@@ -585,7 +590,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
                                               int maxrow, int ntree, int tsize, bool spill = false,
                                               bool midcache = false, bool nobc = false, bool f64arms = false,
                                               bool gl_lists = false, bool treeblk = false, int tmask_words = 0,
-                                              bool gl_stage = false, bool gl_tbr = false) {
+                                              bool gl_stage = false, bool gl_tbr = false, bool f64gl = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -658,13 +663,14 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.sort = take(4 * K);
   L.uctl = take(8 * nu);
   L.scal = take(8 * 4);
-  L.prof = take(8 * FM_NPROF);
+  if (!(spill && gl_stage)) L.prof = take(8 * FM_NPROF);  // (phase clocks: with gl_stage in the global block)
   if (midcache) {
-    L.mcache = take(4 * mc_cap(nv));
+    if (!gl_lists) L.mcache = take(4 * mc_cap(nv));  // a midphase list in the global block is its own cache
     L.mpos = take(tsize * 3 * ncb);
   }
   const bool f64a = f64arms && tsize == 4;
-  if (f64a && !gl_lists) {
+  f64gl = f64a && spill && (gl_lists || f64gl);
+  if (f64a && !f64gl) {
     L.bposd = take(8 * 30 * A);
     L.bRd = take(8 * 90 * A);
   }
@@ -674,15 +680,15 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
     L.H = 0;
     L.c_r = (tsize * (hstride(tsize, nv) * hstride(tsize, nv) + hextra(tsize, nv)) + 15) & ~15;
     int g = L.c_r + ((tsize * CR_N * maxcon + 255) & ~255);
-    if (gl_lists) {  // also the midphase hit list and the float64 arm poses (the (4,16) scene: 4 arenas per CU)
+    if (gl_lists) {  // also the midphase hit list (the (4,16) scene: 4 arenas per CU)
       L.sp = g;
       g += (4 * (ncb * (ncb - 1) / 2) + 255) & ~255;
-      if (f64a) {
-        L.bposd = g;
-        g += 8 * 30 * A;
-        L.bRd = g;
-        g += (8 * 90 * A + 255) & ~255;
-      }
+    }
+    if (f64gl) {  // the float64 arm poses ((4,16); the fp32 IK-class kernels of the other scenes)
+      L.bposd = g;
+      g += 8 * 30 * A;
+      L.bRd = g;
+      g += (8 * 90 * A + 255) & ~255;
     }
     if (gl_tbr) {  // the tree-block solve's coupled system (assembled and factored only on coupled substeps)
       L.tbr = g;
@@ -695,6 +701,8 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
       g += (4 * maxcon + 255) & ~255;
       L.spw = g;
       g += (4 * maxcon + 255) & ~255;
+      L.prof = g;
+      g += (8 * FM_NPROF + 255) & ~255;
     }
     L.gtotal = g;
   }
@@ -733,9 +741,22 @@ struct DimsSpill : Dims {
 #define FM_GL_COLL 1  // round 6: the (2,4) fp64 collision lists in the global block, 145.5k -> 164.3k env-steps/s fp64
 #endif
 #ifndef FM_GL28
-#define FM_GL28 0
+#define FM_GL28 1  // round 6: the fp32 (2,8) collision lists + coupled system in the global block, 193.3k -> 231.4k (config 3)
 #endif
-template <int A_, int K_, bool WIDE_ = false>
+#ifndef FM_GL210
+#define FM_GL210 0
+#endif
+#ifndef FM_GL416
+#define FM_GL416 0
+#endif
+#ifndef FM_TREEBLK24
+#define FM_TREEBLK24 0  // experiment: the (2,4) 64-contact kernel's non-arrowhead substeps through the tree-block solve
+#endif
+#ifndef FM_F64ARMS_IK
+#define FM_F64ARMS_IK 1
+#endif
+// IKK_: the instantiation the IK classes' launches use (the same layout; only DIM::f64arms differs)
+template <int A_, int K_, bool WIDE_ = false, bool IKK_ = false>
 struct FixedDims {
   static constexpr bool fixed = true;
   static constexpr bool spill = FM_SPILL_FIXED && !WIDE_;
@@ -748,10 +769,16 @@ struct FixedDims {
   // the fp32 (4,16) scene (config 5: IK grasps) keeps float64 arm body poses for the narrowphase: a float forward
   // kinematics puts ~1e-7 m on the gripper / arm geoms' positions, which a contact on a cube turns into force errors
   // (tools/fp32_floor.py --probe 64: 1e-7 m of geom noise alone drops the (4,16) Pause toggle to 90 % within)
-  static constexpr bool f64arms = A_ == 4 && K_ == 16;
+  // The IK classes' fp32 kernels of the other scenes too: a grasped cube sits between the gripper plates' contacts,
+  // and the float arm chain's noise drops the (2,4) Pause toggle to 87 % of its env-steps within the SURVEY gate
+  // (worst 0.54) against 100 % for the Backup toggle.  Those poses live in the global block -- both instantiations
+  // share one layout, so the non-IK (benchmark) kernels' LDS is unchanged and they never touch the slots.
+  static constexpr bool f64ik = spill && !WIDE_ && !(A_ == 4 && K_ == 16) && FM_F64ARMS_IK;
+  static constexpr bool f64arms = (A_ == 4 && K_ == 16) || (IKK_ && f64ik);
   // the (4,16) scene also keeps its midphase hit list and float64 arm poses in the global block: 50.0 -> 37.9 KB of
   // LDS, four arenas per CU instead of three
   static constexpr bool gl_lists = spill && A_ == 4 && K_ == 16 && FM_GL_LISTS;
+  static constexpr bool f64gl = gl_lists || f64ik;
   // the collision work lists -- staged contacts, keys, pair words and the midphase list -- in the global block too (the
   // larger side of the phase-local union at (2,4)): FM_GL_COLL=1 the fp64 kernel (29.9 KB of LDS hold 5 arenas per CU),
   // 2 both precisions
@@ -759,13 +786,19 @@ struct FixedDims {
   __host__ __device__ static constexpr bool gl_coll() {
     return spill && !WIDE_ &&
            ((A_ == 2 && K_ == 4 && (FM_GL_COLL == 2 || (FM_GL_COLL == 1 && TS == 8))) ||
-            (A_ == 2 && K_ == 8 && TS == 4 && FM_GL28));
+            gl2x<TS>());
   }
-  // the tree-block solve's coupled system in the global block: with gl_coll, the fp32 (2,8) workspace drops from
-  // 26.7 to ~21 KB of LDS (7 arenas per CU instead of 6)
+  // the fp32 (2,8) / (2,10) / (4,16) kernels: collision lists and the tree-block coupled system in the global block (26.1 ->
+  // 19.0 KB of LDS at (2,8): 8 arenas per CU instead of 6)
+  template <int TS>
+  __host__ __device__ static constexpr bool gl2x() {
+    return spill && !WIDE_ && TS == 4 &&
+           ((A_ == 2 && ((K_ == 8 && FM_GL28) || (K_ == 10 && FM_GL210))) || (A_ == 4 && K_ == 16 && FM_GL416));
+  }
+  // the tree-block solve's coupled system in the global block (assembled and factored only on coupled substeps)
   template <int TS>
   __host__ __device__ static constexpr bool gl_tbr() {
-    return spill && !WIDE_ && treeblk && A_ == 2 && K_ == 8 && TS == 4 && FM_GL28;
+    return spill && !WIDE_ && treeblk_for<TS>() && (gl2x<TS>() || (A_ == 2 && K_ == 4));
   }
   template <int TS>
   __host__ __device__ static constexpr bool gl_sp() {
@@ -780,6 +813,12 @@ struct FixedDims {
   // measured 175.8k vs 189.5k env-steps/s -- the extra code alone costs its register allocation -- and neither the
   // tree-block solve on every substep nor only on heavy substeps (> 8 contacts on a tree) won that back)
   static constexpr bool treeblk = (WIDE_ || (spill && !(A_ == 2 && K_ == 4))) && FM_TREEBLK;
+  // ... and, per precision, the (2,4) 64-contact kernel's non-arrowhead substeps (FM_TREEBLK24: 1 fp32, 2 both)
+  template <int TS>
+  __host__ __device__ static constexpr bool treeblk_for() {
+    return treeblk || (spill && !WIDE_ && A_ == 2 && K_ == 4 && FM_TREEBLK &&
+                       (FM_TREEBLK24 == 2 || (FM_TREEBLK24 == 1 && TS == 4)));
+  }
   static constexpr int phys_stride = 2 * nq + 3 * nv, dbl_stride = nu + 3 + 2 * A_ + 1 + 27 * A_,
                        int_stride = 2 * K_ + I_NINT + (3 + A_) * A_;
   int N, nbox, npair, nparam, frame_skip, maxcon, ncbp, obs_dim, act_dim;  // obs / act dims depend on the env class
@@ -788,8 +827,9 @@ struct FixedDims {
         ncbp(d.ncbp), obs_dim(d.obs_dim), act_dim(d.act_dim) {}
   template <int TS>
   __host__ __device__ static constexpr Lay layout() {
-    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE, f64arms,
-                       gl_sp<TS>(), treeblk, 0, gl_coll<TS>(), gl_tbr<TS>());
+    return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE,
+                       (A_ == 4 && K_ == 16) || f64ik, gl_sp<TS>(), treeblk_for<TS>(), 0, gl_coll<TS>(), gl_tbr<TS>(),
+                       f64gl);
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&
@@ -797,5 +837,9 @@ struct FixedDims {
            d.phys_stride == phys_stride && d.dbl_stride == dbl_stride && d.int_stride == int_stride;
   }
 };
+
+// the IK classes' instantiation: float64 arm poses in the fp32 kernels (FixedDims::f64ik)
+template <typename T, int A, int K>
+using FixedDimsIK = FixedDims<A, K, false, sizeof(T) == 4>;
 
 }  // namespace fm

@@ -229,7 +229,7 @@ struct Ws {
   __device__ __forceinline__ double* bposd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (double*)((DIM::gl_lists ? gbase : base) + c.bposd);
+      return (double*)((DIM::f64gl ? gbase : base) + c.bposd);
     } else {
       return (double*)(base + L->bposd);
     }
@@ -237,7 +237,7 @@ struct Ws {
   __device__ __forceinline__ double* bRd() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (double*)((DIM::gl_lists ? gbase : base) + c.bRd);
+      return (double*)((DIM::f64gl ? gbase : base) + c.bRd);
     } else {
       return (double*)(base + L->bRd);
     }
@@ -545,7 +545,7 @@ struct Ws {
   __device__ __forceinline__ unsigned long long* prof() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (unsigned long long*)(base + c.prof);
+      return (unsigned long long*)((DIM::template gl_coll<sizeof(T)>() ? gbase : base) + c.prof);
     } else {
       return (unsigned long long*)(base + L->prof);
     }
@@ -1551,9 +1551,10 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   // DIM::midcache: the list of an inflated test (every bound + MC_MARGIN) is kept and reused while no moving
   // body has moved MC_HALF since it was built -- a pair outside the inflated test then cannot pass the exact one,
   // and the geom-pair test and narrowphase below decide the contacts as before (so the contact set is unchanged)
-  // the list is built in w.sp() (the arena's global block with DIM::gl_lists, else LDS) and read back from there or,
-  // when the cached list is reused, from w.mcache() (LDS): reads go through address-space-typed pointers chosen per
-  // access, never through one pointer selected between the two (that would be generic: FLAT instructions)
+  // the list is built in w.sp() (the arena's global block with DIM::gl_sp, else LDS) and read back from there or,
+  // when the cached list is reused, from w.mcache() (LDS; w.sp() itself when that is global): reads go through
+  // address-space-typed pointers chosen per access, never through one pointer selected between the two (that would
+  // be generic: FLAT instructions)
   uint32_t* const sp = w.sp();
   constexpr int SPAS = DIM::template gl_sp<sizeof(T)>() ? AS_GLOBAL : AS_LDS;
   int nsp = 0, total = 0;
@@ -1610,9 +1611,11 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
       for (int k = 0; k < NPP; k++)
         if (k * WAVE < dm.ncbp) sweep(bpr[k], k * WAVE + LANE);
       if constexpr (DIM::midcache) {
-        // keep the inflated list (when it fits) and the positions it was built at
-        const bool fits = nsp <= mc_cap(DIM::nv);
-        for (int e = LANE; e < nsp && fits; e += WAVE) w.mcache()[e] = ((const uint32_t FM_AS(SPAS)*)sp)[e];
+        // keep the inflated list (when it fits) and the positions it was built at.  A list built in the global
+        // block stays there (nothing else writes w.sp() until the next rebuild): it is its own cache
+        const bool fits = SPAS == AS_GLOBAL || nsp <= mc_cap(DIM::nv);
+        if constexpr (SPAS != AS_GLOBAL)
+          for (int e = LANE; e < nsp && fits; e += WAVE) w.mcache()[e] = ((const uint32_t FM_AS(SPAS)*)sp)[e];
         for (int b = LANE; b < dm.ncb; b += WAVE) {
           const T* o = w.cbw() + 8 * b;
           T* p0 = w.mpos() + 3 * b;
@@ -1652,7 +1655,7 @@ __device__ __forceinline__ void collide(const Model<T>& M, const Ws<T, DIM>& w, 
   int* mark = misc + 16;  // [64] scratch of the collision phase
   int carry = 0;
   auto sp_at = [&](int i) -> uint32_t {
-    if (DIM::midcache && reuse) return ((const uint32_t FM_AS(AS_LDS)*)w.mcache())[i];
+    if (DIM::midcache && SPAS != AS_GLOBAL && reuse) return ((const uint32_t FM_AS(AS_LDS)*)w.mcache())[i];
     return ((const uint32_t FM_AS(SPAS)*)sp)[i];
   };
   for (int e0 = 0; e0 < total; e0 += WAVE) {
@@ -4350,7 +4353,7 @@ __device__ constexpr bool pc_scene() {
 template <typename T, typename DIM>
 __device__ constexpr bool treeblk_scene() {
   if constexpr (DIM::fixed)
-    return DIM::treeblk;
+    return DIM::template treeblk_for<sizeof(T)>();
   else
     return false;
 }

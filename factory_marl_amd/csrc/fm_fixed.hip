@@ -27,12 +27,19 @@ static_assert(!(FM_A == 2 && FM_K == 4 && FM_PREC == 32 && FM_SPILL_FIXED) ||
                   FixedDims<2, 4>::template layout<4>().total <= 160 * 1024 / 8,
               "(2,4) fp32 workspace above 20 KiB: fewer than 8 arenas per CU");
 
+// the IK classes' kernels run in the handle's layout (FixedDimsIK differs only in DIM::f64arms)
+static_assert(FixedDimsIK<FM_REAL, FM_A, FM_K>::template layout<sizeof(FM_REAL)>().total ==
+                      FixedDims<FM_A, FM_K>::template layout<sizeof(FM_REAL)>().total &&
+                  FixedDimsIK<FM_REAL, FM_A, FM_K>::template layout<sizeof(FM_REAL)>().gtotal ==
+                      FixedDims<FM_A, FM_K>::template layout<sizeof(FM_REAL)>().gtotal,
+              "the IK instantiation's layout differs");
+
 template <typename T, int A, int K>
 hipError_t fixed_set_attr(int lds_bytes) {
   hipError_t e = hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K>, false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)step_kernel<T, FixedDims<A, K>, true>,
+  return hipFuncSetAttribute((const void*)step_kernel<T, FixedDimsIK<T, A, K>, true>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
@@ -40,7 +47,8 @@ hipError_t fixed_set_attr(int lds_bytes) {
 template <typename T, int A, int K>
 void fixed_launch(const StepParams<T>& p, int num_arenas, int lds_bytes, hipStream_t stream, bool ik) {
   if (ik)
-    hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>, true>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
+    hipLaunchKernelGGL((step_kernel<T, FixedDimsIK<T, A, K>, true>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream,
+                       p);
   else
     hipLaunchKernelGGL((step_kernel<T, FixedDims<A, K>, false>), dim3(num_arenas), dim3(WAVE), lds_bytes, stream, p);
 }

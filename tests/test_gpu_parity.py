@@ -366,6 +366,30 @@ def test_teacher_forced_ik_classes_fp64_4x16(oracle, env_class):
 
 
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
+@pytest.mark.parametrize("A_,K_,env_class", [(2, 4, "PauseIKToggleEnv"), (2, 4, "BackupIKToggleEnv"),
+                                             (2, 4, "AllDeltaProgressRewardEnv"), (2, 8, "PauseIKToggleEnv"),
+                                             (2, 10, "BackupIKToggleEnv")])
+def test_fp32_ik_classes_within_survey_gate(oracle, A_, K_, env_class):
+    """the IK classes (grasps: a cube held between the gripper plates' contacts) in the benchmarked fp32 kernels of
+    the 2-arm scenes, 150 teacher-forced env-steps from reset against the float64 oracle and the oracle restepped at
+    MuJoCo's 1e-8 tolerance: integer / IK state exact, the nearer oracle within the SURVEY gate on >= 99 % of the
+    steps and within 5e-3 on every step (the cap of the fp32 (2,8) scene test above; measured round 6: (2,4) Backup
+    step 111 at 4.2e-3 against both oracles, every other step within 1e-4).  Round 6: these kernels take float64 arm
+    poses (FixedDims::f64ik) -- with the float arm chain the (2,4) Pause toggle had 87 % of its steps within, worst
+    0.54 (host backend, same kernel)"""
+    traj = pu.rollout(oracle, A_, K_, 150, seed_actions=3, env_class=env_class)
+    tol8 = pu.restep_at_tolerance(oracle, A_, K_, traj, 1e-8, env_class)
+    r = pu.compare(traj, "fp32", A_, K_, env_class, alt=tol8, verbose_tol=1e-3)
+    e = r["errs"]
+    print(f"fp32 ({A_},{K_}) {env_class} vs the 1e-12 oracle: {np.mean(e <= 1e-4):.1%} within 1e-4, median "
+          f"{np.median(e):.2e}, worst {e.max():.2e}")
+    assert not r["flag_bad"] and not r["int_bad"] and not r["reset_bad"], (r["flag_bad"], r["int_bad"])
+    assert r["counters"][:, 0].sum() == 0
+    within, worst, missing = pu.two_oracle_gate(r, frac=0.99, cap=5e-3)
+    print(f"  nearer of the two oracles: {within:.1%} within 1e-4, worst {worst:.2e}, missing {missing}")
+
+
+@pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 def test_ik_timing_follows_control_frequency_and_pt_time(oracle):
     """ik_policy.py:56-67 derives the IK policy's step counts (release 0.5 s, grasp 1 s, move 1 s, timeout 3 s) and its
     velocity compensation (pt_time * dt * 15) from env.dt and env.pt_time: at control_frequency 20 Hz (frame_skip 50:
