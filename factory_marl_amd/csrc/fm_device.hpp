@@ -6007,6 +6007,7 @@ __device__ __forceinline__ void step_arena(char* smem, const int arena) {
     refresh_copies(M, w);
     for (int i = LANE; i < dm.nq; i += WAVE) phw[dm.nq + dm.nv + i] = w.qd()[i];
     for (int i = LANE; i < dm.nv; i += WAVE) phw[2 * dm.nq + dm.nv + i] = w.vd()[i];
+    SYNC();  // the reset pass's stage reads the float copies other lanes just wrote (tools/lds_race_check.py)
     reset_pass = true;
   }
   store_state(M, S, w, arena);

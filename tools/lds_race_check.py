@@ -18,7 +18,8 @@ FM_RERUN_AT_50): build the detector library with them.
 
 usage: make -C factory_marl_amd/csrc race OBJDIR=build_race XDEFS=-DFM_EXPERIMENTS=1   (builds scratch/lib_race.so)
        FACTORYSIM_LIB=scratch/lib_race.so python tools/lds_race_check.py
-       [RACE_STEPS=n] [RACE_CASES=i,j] [RACE_PRECISIONS=fp64,fp32]   (a case takes minutes: run cases in parallel)"""
+       [RACE_STEPS=n] [RACE_CASES=i,j] [RACE_PRECISIONS=fp64,fp32]   (a case takes minutes: run cases in parallel)
+       [RACE_TRAJ=A,K,T,seed,EnvClass [RACE_PICK=lo:hi]]   (a parity test's teacher-forced launch instead)"""
 import ctypes as C
 import os
 import subprocess
@@ -41,9 +42,29 @@ def main():
              ("AllFullRLProgressRewardEnv", 2, 4, "FM_RERUN_AT_50=1"), ("PauseIKToggleEnv", 2, 4, "FM_FORCE_RERUN=1"),
              ("AllFullRLProgressRewardEnv", 2, 8, "FM_NO_TREEBLK=1")]
     steps = int(os.environ.get("RACE_STEPS", "3"))
+    if os.environ.get("RACE_TRAJ"):
+        # A,K,T,seed,EnvClass: the records of an oracle rollout stepped teacher-forced in one launch (a GPU parity
+        # test's launch, e.g. one that faulted on the GPU)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import parity_util as pu
+        from oracle import pyoracle
+
+        pyoracle.build()
+        sp = os.environ["RACE_TRAJ"].split(",")
+        A_, K_, T_, seed = map(int, sp[:4])
+        tr = pu.rollout(pyoracle, A_, K_, T_, seed_actions=seed, env_class=sp[4])
+        pick = os.environ.get("RACE_PICK")  # a subset of the records: lo:hi
+        if pick:
+            lo, hi = map(int, pick.split(":"))
+            tr = tuple(x[lo:hi] for x in tr)
+        for prec in os.environ.get("RACE_PRECISIONS", "fp32").split(","):
+            s = pu.summary(pu.compare(tr, prec, A_, K_, sp[4], device="cpu"))
+            print(f"ran {prec} {sp[4]} ({A_},{K_}) teacher-forced x {len(tr[0])}: within {s['within']}, worst "
+                  f"{s['worst']:.2e}", flush=True)
+        cases = []
     if os.environ.get("RACE_CASES"):
         cases = [cases[int(i)] for i in os.environ["RACE_CASES"].split(",")]
-    for prec in os.environ.get("RACE_PRECISIONS", "fp64,fp32").split(","):
+    for prec in os.environ.get("RACE_PRECISIONS", "fp64,fp32").split(",") if cases else []:
         for cls, A, K, exp in cases:
             env = FactoryVecEnv(1, env_class=cls, env_kwargs=run_kwargs(cls, num_arms=A, max_num_objects=K, seed=42),
                                 device="cpu", precision=prec, experimental=bool(exp))
