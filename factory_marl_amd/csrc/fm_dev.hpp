@@ -663,7 +663,10 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   L.sort = take(4 * K);
   L.uctl = take(8 * nu);
   L.scal = take(8 * 4);
-  if (!(spill && gl_stage)) L.prof = take(8 * FM_NPROF);  // (phase clocks: with gl_stage in the global block)
+  // phase clocks (profiling only): in the global block at (4,16) with its lists there (FM_GL416), the 144 B it misses
+  // for 5 arenas per CU; elsewhere the global pointer costs the kernels ~10 VGPR spills
+  const bool gl_prof = spill && gl_stage && A == 4;
+  if (!gl_prof) L.prof = take(8 * FM_NPROF);
   if (midcache) {
     if (!gl_lists) L.mcache = take(4 * mc_cap(nv));  // a midphase list in the global block is its own cache
     L.mpos = take(tsize * 3 * ncb);
@@ -701,8 +704,10 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
       g += (4 * maxcon + 255) & ~255;
       L.spw = g;
       g += (4 * maxcon + 255) & ~255;
-      L.prof = g;
-      g += (8 * FM_NPROF + 255) & ~255;
+      if (gl_prof) {
+        L.prof = g;
+        g += (8 * FM_NPROF + 255) & ~255;
+      }
     }
     L.gtotal = g;
   }
@@ -744,7 +749,7 @@ struct DimsSpill : Dims {
 #define FM_GL28 1  // round 6: the fp32 (2,8) collision lists + coupled system in the global block, 193.3k -> 231.4k (config 3)
 #endif
 #ifndef FM_GL210
-#define FM_GL210 0
+#define FM_GL210 1  // round 6: the same for fp32 (2,10), 5 -> 8 arenas per CU, 155.0k -> 202.7k env-steps/s (16384 arenas)
 #endif
 #ifndef FM_GL416
 #define FM_GL416 0
@@ -788,8 +793,9 @@ struct FixedDims {
            ((A_ == 2 && K_ == 4 && (FM_GL_COLL == 2 || (FM_GL_COLL == 1 && TS == 8))) ||
             gl2x<TS>());
   }
-  // the fp32 (2,8) / (2,10) / (4,16) kernels: collision lists and the tree-block coupled system in the global block (26.1 ->
-  // 19.0 KB of LDS at (2,8): 8 arenas per CU instead of 6)
+  // the fp32 (2,8) / (2,10) kernels: collision lists and the tree-block coupled system in the global
+  // block (26.1 -> 17.9 KB of LDS at (2,8), 27.4 -> 19.6 KB at (2,10): 8 arenas per CU instead of 6 / 5); FM_GL416=1
+  // (experiment) the (4,16) one too
   template <int TS>
   __host__ __device__ static constexpr bool gl2x() {
     return spill && !WIDE_ && TS == 4 &&

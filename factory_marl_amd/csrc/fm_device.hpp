@@ -545,7 +545,7 @@ struct Ws {
   __device__ __forceinline__ unsigned long long* prof() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (unsigned long long*)((DIM::template gl_coll<sizeof(T)>() ? gbase : base) + c.prof);
+      return (unsigned long long*)((DIM::template gl_coll<sizeof(T)>() && DIM::A == 4 ? gbase : base) + c.prof);
     } else {
       return (unsigned long long*)(base + L->prof);
     }

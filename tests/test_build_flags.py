@@ -152,7 +152,8 @@ def test_product_library_rejects_experiment_switches():
 
 # VGPR spill ceilings of every step-kernel instantiation of the product library (code-object notes, round 6): the
 # benchmark kernel has none; the two-waves-per-SIMD kernels of (2,4) fp64 / IK classes and (2,8) / (2,10) AllFullRL
-# trade their spills for occupancy (measured: DESIGN.md §4 / §4c); the one-wave kernels keep only the few VGPRs the
+# trade their spills for occupancy (measured: DESIGN.md §4 / §4c; the (2,10) one, 893 spilled at 8 arenas per CU,
+# measured faster than an allocation of the same code with 180, profiles/r06r_ab/); the one-wave kernels keep only the few VGPRs the
 # non-inlined IK calls save.  A change that spills more than this is a regression to measure before it ships.
 SPILL_CEILING = {
     "float, fm::FixedDims<2, 4, false, false>, false": 0,
@@ -165,7 +166,7 @@ SPILL_CEILING = {
     "float, fm::FixedDims<2, 8, false, true>, true": 8,
     "double, fm::FixedDims<2, 8, false, false>, false": 130,
     "double, fm::FixedDims<2, 8, false, false>, true": 8,
-    "float, fm::FixedDims<2, 10, false, false>, false": 193,
+    "float, fm::FixedDims<2, 10, false, false>, false": 900,
     "float, fm::FixedDims<2, 10, false, true>, true": 8,
     "double, fm::FixedDims<2, 10, false, false>, false": 135,
     "double, fm::FixedDims<2, 10, false, false>, true": 8,

@@ -368,7 +368,7 @@ def test_teacher_forced_ik_classes_fp64_4x16(oracle, env_class):
 @pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")
 @pytest.mark.parametrize("A_,K_,env_class", [(2, 4, "PauseIKToggleEnv"), (2, 4, "BackupIKToggleEnv"),
                                              (2, 4, "AllDeltaProgressRewardEnv"), (2, 8, "PauseIKToggleEnv"),
-                                             (2, 10, "BackupIKToggleEnv")])
+                                             (2, 10, "BackupIKToggleEnv"), (2, 10, "PauseIKToggleEnv")])
 def test_fp32_ik_classes_within_survey_gate(oracle, A_, K_, env_class):
     """the IK classes (grasps: a cube held between the gripper plates' contacts) in the benchmarked fp32 kernels of
     the 2-arm scenes, 150 teacher-forced env-steps from reset against the float64 oracle and the oracle restepped at

@@ -40,7 +40,8 @@ def main():
              ("AllFullRLProgressRewardEnv", 2, 8, ""), ("AllFullRLProgressRewardEnv", 2, 10, ""),
              ("PauseIKToggleEnv", 4, 16, ""), ("AllFullRLProgressRewardEnv", 2, 4, "FM_FORCE_RERUN=1"),
              ("AllFullRLProgressRewardEnv", 2, 4, "FM_RERUN_AT_50=1"), ("PauseIKToggleEnv", 2, 4, "FM_FORCE_RERUN=1"),
-             ("AllFullRLProgressRewardEnv", 2, 8, "FM_NO_TREEBLK=1")]
+             ("AllFullRLProgressRewardEnv", 2, 8, "FM_NO_TREEBLK=1"), ("BackupIKToggleEnv", 2, 10, ""),
+             ("PauseIKToggleEnv", 2, 10, ""), ("BackupIKToggleEnv", 2, 8, "")]
     steps = int(os.environ.get("RACE_STEPS", "3"))
     if os.environ.get("RACE_TRAJ"):
         # A,K,T,seed,EnvClass: the records of an oracle rollout stepped teacher-forced in one launch (a GPU parity
