@@ -89,6 +89,10 @@ struct Dims {
     return false;
   }
   template <int TS>
+  __host__ __device__ static constexpr bool gl_gx() {
+    return false;
+  }
+  template <int TS>
   __host__ __device__ static constexpr bool gl_sp() {
     return false;
   }
@@ -590,7 +594,8 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
                                               int maxrow, int ntree, int tsize, bool spill = false,
                                               bool midcache = false, bool nobc = false, bool f64arms = false,
                                               bool gl_lists = false, bool treeblk = false, int tmask_words = 0,
-                                              bool gl_stage = false, bool gl_tbr = false, bool f64gl = false) {
+                                              bool gl_stage = false, bool gl_tbr = false, bool f64gl = false,
+                                              bool gl_gx = false) {
   Lay L{};
   int off = 0;
   auto take = [&off](int bytes) {
@@ -641,7 +646,7 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
   if (treeblk) L.tblk = take(tsize * tb_floats(ntree, gl_tbr));
   int uend = off;
   off = u0;
-  L.gx = take(tsize * 4 * ngc);
+  if (!gl_gx) L.gx = take(tsize * 4 * ngc);
   L.cbw = take(tsize * 8 * ncb);
   if (!gl_lists) L.sp = take(4 * (ncb * (ncb - 1) / 2));  // every possible body pair can pass the midphase
   L.gsurv = take(4 * 4 * WAVE);
@@ -696,6 +701,10 @@ __host__ __device__ constexpr Lay make_layout(int A, int K, int nq, int nv, int 
     if (gl_tbr) {  // the tree-block solve's coupled system (assembled and factored only on coupled substeps)
       L.tbr = g;
       g += (tsize * TB_MAXR * TB_MAXR + 255) & ~255;
+    }
+    if (gl_gx && spill) {  // the geom centres (the largest array left on the collision side of the union)
+      L.gx = g;
+      g += (tsize * 4 * ngc + 255) & ~255;
     }
     if (gl_stage) {  // the staged contacts, their keys and pair words (the collision side of the phase-local union)
       L.stage = g;
@@ -754,6 +763,9 @@ struct DimsSpill : Dims {
 #ifndef FM_GL416
 #define FM_GL416 0
 #endif
+#ifndef FM_GL_GX
+#define FM_GL_GX 0
+#endif
 #ifndef FM_TREEBLK24
 #define FM_TREEBLK24 0  // experiment: the (2,4) 64-contact kernel's non-arrowhead substeps through the tree-block solve
 #endif
@@ -806,6 +818,11 @@ struct FixedDims {
   __host__ __device__ static constexpr bool gl_tbr() {
     return spill && !WIDE_ && treeblk_for<TS>() && (gl2x<TS>() || (A_ == 2 && K_ == 4));
   }
+  // experiment: the fp64 (2,4) kernel's geom centres in the global block too (22.7 -> 18.7 KB: 8 arenas per CU)
+  template <int TS>
+  __host__ __device__ static constexpr bool gl_gx() {
+    return spill && !WIDE_ && A_ == 2 && K_ == 4 && TS == 8 && FM_GL_GX;
+  }
   template <int TS>
   __host__ __device__ static constexpr bool gl_sp() {
     return gl_lists || gl_coll<TS>();
@@ -835,7 +852,7 @@ struct FixedDims {
   __host__ __device__ static constexpr Lay layout() {
     return make_layout(A, K, nq, nv, nu, ngc, ncb, MAXC, maxrow, ntree, TS, spill, midcache, MAXC == WAVE,
                        (A_ == 4 && K_ == 16) || f64ik, gl_sp<TS>(), treeblk_for<TS>(), 0, gl_coll<TS>(), gl_tbr<TS>(),
-                       f64gl);
+                       f64gl, gl_gx<TS>());
   }
   static bool matches(const Dims& d) {
     return d.A == A && d.K == K && d.nq == nq && d.nv == nv && d.nu == nu && d.ngc == ngc && d.ncb == ncb &&

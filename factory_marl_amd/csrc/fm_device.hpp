@@ -365,7 +365,7 @@ struct Ws {
   __device__ __forceinline__ T* gx() const {
     if constexpr (DIM::fixed && !FM_WS_RUNTIME_LAYOUT) {
       constexpr Lay c = DIM::template layout<sizeof(T)>();
-      return (T*)(base + c.gx);
+      return (T*)((DIM::template gl_gx<sizeof(T)>() ? gbase : base) + c.gx);
     } else {
       return (T*)(base + L->gx);
     }
