@@ -764,7 +764,7 @@ struct DimsSpill : Dims {
 #define FM_GL416 0
 #endif
 #ifndef FM_GL_GX
-#define FM_GL_GX 0
+#define FM_GL_GX 1  // round 6: fp64 (2,4) 7 -> 8 arenas per CU, 167.5k -> 191.5k env-steps/s (profiles/r06t_glgx_ab/)
 #endif
 #ifndef FM_TREEBLK24
 #define FM_TREEBLK24 0  // experiment: the (2,4) 64-contact kernel's non-arrowhead substeps through the tree-block solve
@@ -818,7 +818,7 @@ struct FixedDims {
   __host__ __device__ static constexpr bool gl_tbr() {
     return spill && !WIDE_ && treeblk_for<TS>() && (gl2x<TS>() || (A_ == 2 && K_ == 4));
   }
-  // experiment: the fp64 (2,4) kernel's geom centres in the global block too (22.7 -> 18.7 KB: 8 arenas per CU)
+  // the fp64 (2,4) kernel's geom centres in the global block too (22.7 -> 18.7 KB: 8 arenas per CU)
   template <int TS>
   __host__ __device__ static constexpr bool gl_gx() {
     return spill && !WIDE_ && A_ == 2 && K_ == 4 && TS == 8 && FM_GL_GX;
